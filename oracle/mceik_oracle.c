@@ -1,0 +1,357 @@
+/* mceik_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's hot path, used solely as the CHECKER by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  Nothing in
+ * mceik_amd/ links, loads or calls this file; the product fails loudly when its
+ * HIP library is missing instead of falling back here.
+ *
+ * Contents (reference file:line followed by each piece):
+ *   - eikonal serial solve, fp64 and fp32 twins (fsm_impl.inc; fsm3d.f90:28-99,
+ *     419-840, 1968-2052)
+ *   - L2 grid-search misfit with analytic origin time (locate.c:388-567,923-1047)
+ *   - Fortran grid-search variant (gridsearch.f90:176-329,382-456), for the
+ *     reference's own known-answer test (optimum 21124, t0 ~ 4 s)
+ *   - Philox4x32-10, deterministic log, proposal and Metropolis step: the
+ *     reference defines no MCMC (include/mceik.h:1-14 is empty), so these restate
+ *     the build's own definition; parity there is between
+ *     this file and the HIP kernels, not with the reference.
+ * Build: gcc -O2 -ffp-contract=off -fopenmp (oracle/Makefile).  Pinned against
+ * the compiled reference by tests/golden (tests/golden/make_golden.py).
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* EIKONAL_SOURCE_INDEX (fsm3d.f90:697-711); returns a 1-based index. */
+static int oracle_source_index(int nx, double x0, double dx, double xs)
+{
+    if (xs <= x0) return 1;
+    if (xs >= x0 + (double)(nx - 1) * dx) return nx;
+    return (int)((xs - x0) / dx + 0.5) + 1;
+}
+
+/* EIKONAL_INIT_GRID (fsm3d.f90:716-755).  Note the reference's quirks: an
+ * on-node source always includes isx-1 (so isx=1 is an error) and includes
+ * isx+1 only when isx < nx-1. */
+static int oracle_init_grid(int nx, int isx, double x0, double dx, double xs, int loc[3])
+{
+    int np = 0, ierr = 0;
+    loc[0] = loc[1] = loc[2] = -1;
+    double xe = x0 + (double)(isx - 1) * dx;
+    if (xe > xs)      { loc[0] = isx - 1; loc[1] = isx; np = 2; }
+    else if (xe < xs) { loc[0] = isx; loc[1] = isx + 1; np = 2; }
+    else {
+        if (isx > 0) loc[np++] = isx - 1;
+        loc[np++] = isx;
+        if (isx < nx - 1) loc[np++] = isx + 1;
+    }
+    for (int i = 0; i < np; i++) if (loc[i] < 1 || loc[i] > nx) ierr = 1;
+    return ierr;
+}
+
+/* ---- fp64 twin (bitwise the reference) ---- */
+#define REAL double
+#define FN(x) x##_f64
+#define RC(x) (x)
+#define UNAN DBL_MAX
+#define SQRT sqrt
+#define FABS fabs
+#define THIRD (1.0 / 3.0)
+#define TWO_THIRD (2.0 / 3.0)
+#include "fsm_impl.inc"
+#undef REAL
+#undef FN
+#undef RC
+#undef UNAN
+#undef SQRT
+#undef FABS
+#undef THIRD
+#undef TWO_THIRD
+
+/* ---- fp32 twin (bitwise the HIP fp32 kernel) ---- */
+#define REAL float
+#define FN(x) x##_f32
+#define RC(x) ((float)(x))
+#define UNAN FLT_MAX
+#define SQRT sqrtf
+#define FABS fabsf
+#define THIRD (1.0f / 3.0f)
+#define TWO_THIRD (2.0f / 3.0f)
+#define STABLE_UPDATE 1
+#include "fsm_impl.inc"
+#undef REAL
+#undef FN
+#undef RC
+#undef UNAN
+#undef SQRT
+#undef FABS
+#undef THIRD
+#undef TWO_THIRD
+#undef STABLE_UPDATE
+
+/* Batched fp64 solves for the CPU baseline: one (model, station) solve per
+ * OpenMP thread, no nested parallelism -- the reference's table-parallel design
+ * (mpiutils.f90:147-149: one serial solve per rank in inter_table_comm). */
+int oracle_batch_solve_f64(int nsolve, int maxit, int nx, int ny, int nz, double tol,
+                           double h, double x0, double y0, double z0,
+                           const double *xs, const double *ys, const double *zs,
+                           const double *slow, const int *slow_index, double *u_out,
+                           int keep_fields, int nthreads)
+{
+    size_t n = (size_t)nx * ny * nz;
+    int nerr = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nerr)
+#endif
+    for (int s = 0; s < nsolve; s++) {
+        double ts = 0.0;
+        double *u = keep_fields ? u_out + (size_t)s * n : (double *)malloc(n * sizeof(double));
+        const double *sl = slow + (size_t)slow_index[s] * n;
+        int it;
+        nerr += oracle_eikonal3d_solve_f64(maxit, 1, nx, ny, nz, tol, h, x0, y0, z0,
+                                           &ts, &xs[s], &ys[s], &zs[s], sl, u, &it) != 0;
+        if (!keep_fields) { u_out[s] = u[0]; free(u); }
+    }
+    return nerr;
+}
+
+/* ---------------- L2 misfit (locate.c:923-1047) ---------------- */
+int oracle_locate_l2_gridsearch_f64(int ldgrd, int ngrd, int nobs, int iwantOT, double t0use,
+                                    const int *mask, const double *tobs, const double *tcorr,
+                                    const double *varobs, const double *test,
+                                    double *t0, double *objfn)
+{
+    if (ldgrd < ngrd || nobs < 1 || !mask || !tobs || !varobs || !test || !t0 || !objfn)
+        return 1;
+    for (int g = 0; g < ngrd; g++) objfn[g] = 0.0;
+    int *use = (int *)malloc(sizeof(int) * nobs);
+    double *tc = (double *)malloc(sizeof(double) * nobs), *wt = (double *)malloc(sizeof(double) * nobs);
+    int nuse = 0;
+    double xnorm = 0.0;
+    for (int i = 0; i < nobs; i++) {
+        if (mask[i] != 0) continue;
+        tc[nuse] = tcorr ? tobs[i] - tcorr[i] : tobs[i];
+        use[nuse] = i;
+        wt[nuse] = 1.0 / varobs[i];
+        xnorm = xnorm + wt[nuse];
+        nuse++;
+    }
+    if (iwantOT == 1) {
+        for (int g = 0; g < ngrd; g++) t0[g] = 0.0;
+        for (int j = 0; j < nuse; j++) {
+            double w = wt[j] / xnorm, to = tc[j];
+            const double *te = test + (size_t)ldgrd * use[j];
+            for (int g = 0; g < ngrd; g++) t0[g] = t0[g] + w * (to - te[g]);
+        }
+    } else {
+        for (int g = 0; g < ngrd; g++) t0[g] = t0use;
+    }
+    const double sqrt2i = 0.7071067811865475;
+    for (int j = 0; j < nuse; j++) {
+        double w = wt[j] * sqrt2i, to = tc[j];
+        const double *te = test + (size_t)ldgrd * use[j];
+        for (int g = 0; g < ngrd; g++) {
+            double res = w * (to - (te[g] + t0[g]));
+            objfn[g] = objfn[g] + res * res;
+        }
+    }
+    free(use); free(tc); free(wt);
+    return 0;
+}
+
+/* Fortran variant (gridsearch.f90:382-456): t0 weight 1/(var_i * sum var),
+ * logPDF weight sqrt(1/2)/var_i.  Returns the 0-based argmin (MINLOC). */
+int oracle_gridsearch_f90_f64(int ldgrd, int ngrd, int nobs, int iwantOT, const int *mask,
+                              const double *tobs, const double *varobs, const double *test,
+                              double *logpdf, double *t0_at_opt)
+{
+    double *t0 = (double *)calloc((size_t)ngrd, sizeof(double));
+    for (int g = 0; g < ngrd; g++) logpdf[g] = 0.0;
+    if (iwantOT == 1) {
+        double xnorm = 0.0;
+        for (int i = 0; i < nobs; i++) if (mask[i] != 1) xnorm = xnorm + varobs[i];
+        for (int i = 0; i < nobs; i++) {
+            if (mask[i] == 1) continue;
+            double wt = 1.0 / (varobs[i] * xnorm), to = tobs[i];
+            const double *te = test + (size_t)ldgrd * i;
+            for (int g = 0; g < ngrd; g++) t0[g] = t0[g] + wt * (to - te[g]);
+        }
+    }
+    const double sqrt2i = 1.0 / sqrt(2.0);
+    for (int i = 0; i < nobs; i++) {
+        if (mask[i] == 1) continue;
+        double wt = sqrt2i / varobs[i], to = tobs[i];
+        const double *te = test + (size_t)ldgrd * i;
+        for (int g = 0; g < ngrd; g++) {
+            double res = wt * (to - (te[g] + t0[g]));
+            logpdf[g] = logpdf[g] + res * res;
+        }
+    }
+    int iopt = 0;
+    for (int g = 1; g < ngrd; g++) if (logpdf[g] < logpdf[iopt]) iopt = g;
+    if (t0_at_opt) *t0_at_opt = t0[iopt];
+    free(t0);
+    return iopt;
+}
+
+/* ---------------- MCMC restatement (build-defined) ---------- */
+void oracle_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
+{
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Natural log from IEEE +,-,*,/ only, so host and device agree bit for bit
+ * (both compiled with -ffp-contract=off).  Domain: finite x > 0. */
+double oracle_det_log(double x)
+{
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    b = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+    double m;
+    memcpy(&m, &b, 8);
+    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+    double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double p = 1.0 / 25.0;
+    p = p * s2 + 1.0 / 23.0; p = p * s2 + 1.0 / 21.0; p = p * s2 + 1.0 / 19.0;
+    p = p * s2 + 1.0 / 17.0; p = p * s2 + 1.0 / 15.0; p = p * s2 + 1.0 / 13.0;
+    p = p * s2 + 1.0 / 11.0; p = p * s2 + 1.0 / 9.0;  p = p * s2 + 1.0 / 7.0;
+    p = p * s2 + 1.0 / 5.0;  p = p * s2 + 1.0 / 3.0;  p = p * s2 + 1.0;
+    double de = (double)e;
+    return de * 6.93147180369123816490e-01 + (2.0 * s * p + de * 1.90821492927058770002e-10);
+}
+
+typedef struct {
+    int nx, ny, nz, nrx, nry, nrz, ncx, ncy, ncz, maxit;
+    double h, x0, y0, z0, tol;
+    int nstat, nevents;
+    const double *sx, *sy, *sz;   /* station coordinates = eikonal sources */
+    const int *ev_node;           /* event nearest-node linear index (x fastest) */
+    const int *obs_ptr;           /* CSR [nevents+1], 0-based */
+    const int *obs_stat;          /* 0-based station of each observation */
+    const int *obs_mask;          /* 1 = excluded (locate.c:981-1013 mask) */
+    const double *tobs, *tcorr, *var;
+    int vmin, vmax, dvmax;
+    uint32_t seed;
+} oracle_mcmc_problem;
+
+void oracle_expand_slowness(const oracle_mcmc_problem *p, const int *v, float *slow)
+{
+    for (int iz = 0; iz < p->nz; iz++)
+        for (int iy = 0; iy < p->ny; iy++)
+            for (int ix = 0; ix < p->nx; ix++) {
+                int c = ((iz / p->nrz) * p->ncy + iy / p->nry) * p->ncx + ix / p->nrx;
+                slow[((size_t)iz * p->ny + iy) * p->nx + ix] = 1.0f / (float)v[c];
+            }
+}
+
+/* travel-time table [station][event] (fp32) for one velocity model */
+int oracle_forward_f32(const oracle_mcmc_problem *p, const int *v, float *ttab, int *niter)
+{
+    size_t n = (size_t)p->nx * p->ny * p->nz;
+    float *slow = (float *)malloc(n * sizeof(float));
+    oracle_expand_slowness(p, v, slow);
+    int nerr = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nerr)
+#endif
+    for (int s = 0; s < p->nstat; s++) {
+        float *u = (float *)malloc(n * sizeof(float));
+        double ts = 0.0;
+        int it = 0;
+        nerr += oracle_eikonal3d_solve_f32(p->maxit, 1, p->nx, p->ny, p->nz, p->tol, p->h,
+                                           p->x0, p->y0, p->z0, &ts, &p->sx[s], &p->sy[s],
+                                           &p->sz[s], slow, u, &it) != 0;
+        if (niter) niter[s] = it;
+        for (int e = 0; e < p->nevents; e++) ttab[(size_t)s * p->nevents + e] = u[p->ev_node[e]];
+        free(u);
+    }
+    free(slow);
+    return nerr;
+}
+
+/* logL = -sum_e objfn_e, objfn_e = locate.c L2 with analytic t0 at the
+ * event's node (one grid point, iwantOT = 1), observations in CSR order. */
+double oracle_loglik(const oracle_mcmc_problem *p, const float *ttab)
+{
+    double logl = 0.0;
+    const double sqrt2i = 0.7071067811865475;
+    for (int e = 0; e < p->nevents; e++) {
+        int j0 = p->obs_ptr[e], j1 = p->obs_ptr[e + 1];
+        double xnorm = 0.0, t0 = 0.0, obj = 0.0;
+        for (int j = j0; j < j1; j++) if (!p->obs_mask[j]) xnorm = xnorm + 1.0 / p->var[j];
+        for (int j = j0; j < j1; j++) {
+            if (p->obs_mask[j]) continue;
+            double te = (double)ttab[(size_t)p->obs_stat[j] * p->nevents + e];
+            double tc = p->tobs[j] - p->tcorr[j];
+            t0 = t0 + ((1.0 / p->var[j]) / xnorm) * (tc - te);
+        }
+        for (int j = j0; j < j1; j++) {
+            if (p->obs_mask[j]) continue;
+            double te = (double)ttab[(size_t)p->obs_stat[j] * p->nevents + e];
+            double tc = p->tobs[j] - p->tcorr[j];
+            double res = ((1.0 / p->var[j]) * sqrt2i) * (tc - (te + t0));
+            obj = obj + res * res;
+        }
+        logl = logl - obj;
+    }
+    return logl;
+}
+
+void oracle_propose(const oracle_mcmc_problem *p, uint32_t chain, uint64_t step,
+                    const int *v, int *cell, int *vnew, int *in_prior, double *logu)
+{
+    uint32_t ctr[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0u, 0u}, key[2] = {chain, p->seed}, r[4];
+    oracle_philox4x32_10(ctr, key, r);
+    uint32_t ncell = (uint32_t)(p->ncx * p->ncy * p->ncz);
+    int c = (int)(((uint64_t)r[0] * ncell) >> 32);
+    int mag = 1 + (int)(((uint64_t)r[1] * (uint32_t)p->dvmax) >> 32);
+    int vn = v[c] + ((r[2] & 1u) ? -mag : mag);
+    *cell = c; *vnew = vn;
+    *in_prior = (vn >= p->vmin && vn <= p->vmax);
+    *logu = oracle_det_log(((double)r[3] + 0.5) * (1.0 / 4294967296.0));
+}
+
+/* Runs nsteps Metropolis steps for nchains chains (global ids gid0..); v is
+ * [nchains][ncell] in/out, logl [nchains] in/out; accept [nsteps][nchains]. */
+void oracle_mcmc_run(const oracle_mcmc_problem *p, int nchains, uint32_t gid0, uint64_t step0,
+                     int nsteps, int *v, double *logl, unsigned char *accept, double *logl_trace)
+{
+    size_t ncell = (size_t)p->ncx * p->ncy * p->ncz;
+    int *vp = (int *)malloc(ncell * sizeof(int));
+    float *tt = (float *)malloc(sizeof(float) * p->nstat * p->nevents);
+    for (int st = 0; st < nsteps; st++) {
+        for (int c = 0; c < nchains; c++) {
+            int *vc = v + (size_t)c * ncell;
+            int cell, vn, inp;
+            double logu;
+            oracle_propose(p, gid0 + (uint32_t)c, step0 + (uint64_t)st, vc, &cell, &vn, &inp, &logu);
+            double ln = -HUGE_VAL;
+            if (inp) {          /* outside the prior: rejected without a forward */
+                memcpy(vp, vc, ncell * sizeof(int));
+                vp[cell] = vn;
+                oracle_forward_f32(p, vp, tt, NULL);
+                ln = oracle_loglik(p, tt);
+            }
+            int acc = inp && (logu < ln - logl[c]);
+            if (acc) { vc[cell] = vn; logl[c] = ln; }
+            accept[(size_t)st * nchains + c] = (unsigned char)acc;
+            if (logl_trace) logl_trace[(size_t)st * nchains + c] = logl[c];
+        }
+    }
+    free(vp); free(tt);
+}
