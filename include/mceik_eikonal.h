@@ -1,0 +1,82 @@
+/*
+ * mceik_eikonal.h -- eikonal / misfit entry points of libmceik_hip.so (gfx950).
+ *
+ * The first group is a drop-in for the reference's Fortran BIND(C) symbols:
+ * same names, every argument by pointer, caller-owned host arrays, ierr out.
+ * The batched group is new: device pointers, many solves per launch.
+ */
+#ifndef MCEIK_EIKONAL_H_AMD
+#define MCEIK_EIKONAL_H_AMD 1
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Replaces EIKONAL3D_SERIAL_DRIVER (fsm3d.f90:1968-2052).
+ * job 1: initialise (ierr=1 if already initialised); job 2: solve (ierr=1 if
+ * not initialised; ierr from SETBCS / FSM as the reference); other: finalise.
+ * Computes on the GPU in fp64 with the reference's arithmetic: u is bitwise
+ * equal to the reference's output.  slow, u: [nx*ny*nz], x fastest. */
+void eikonal3d_serial_driver(const int *job, const int *iverb, const int *maxit, const int *nsrc,
+                             const int *nx, const int *ny, const int *nz, const double *tol,
+                             const double *h, const double *x0, const double *y0, const double *z0,
+                             const double *ts, const double *xs, const double *ys, const double *zs,
+                             const double *slow, double *u, int *ierr);
+
+/* Same contract computed in fp32 with the cancellation-free update
+ * (DESIGN.md s.5): |u - u_ref| <= 1e-6 u_ref + 1e-7 s. */
+void eikonal3d_serial_driver_sp(const int *job, const int *iverb, const int *maxit, const int *nsrc,
+                                const int *nx, const int *ny, const int *nz, const double *tol,
+                                const double *h, const double *x0, const double *y0, const double *z0,
+                                const double *ts, const double *xs, const double *ys, const double *zs,
+                                const double *slow, double *u, int *ierr);
+
+/* Replaces locate_l2_gridSearch__double64 (locate.c:923-1047): same
+ * arguments, errors and results (bitwise); host arrays, computed on the GPU.
+ * test: [nobs][ldgrd]; tcorr may be NULL. */
+int locate_l2_gridSearch__double64(int ldgrd, int ngrd, int nobs, int iwantOT, double t0use,
+                                   const int *mask, const double *tobs, const double *tcorr,
+                                   const double *varobs, const double *test,
+                                   double *t0, double *objfn);
+
+/* ---- batched solves on device memory ---------------------------------- */
+typedef struct mceik_fsm_batch {
+    int nx, ny, nz;             /* grid nodes, dx = dy = dz = h              */
+    double h, x0, y0, z0;
+    int maxit;
+    double tol;
+    int precision;              /* 32 or 64                                  */
+    int nmodel, nstat, nsrc;    /* solves = nmodel * nstat                   */
+    const double *src;          /* device [nstat][nsrc][4] = (ts, xs, ys, zs) */
+    int slow_mode;              /* 0: per-node field, 1: inversion grid      */
+    const void *slow;           /* mode 0: device [nmodel][nx*ny*nz] (fp32/fp64 as precision,
+                                   x fastest); mode 1: device float [nmodel][ncell] */
+    int nrx, nry, nrz;          /* mode 1: refinement (cell = node / nr)     */
+    int nev;                    /* events to sample (0: none)                */
+    const int *ev_node;         /* device [nev], x-fastest node index         */
+    float *ttab;                /* device [nmodel*nstat][nev]                */
+    void *u_out;                /* device [nmodel*nstat][nx*ny*nz] or NULL   */
+    int *niter, *ierr;          /* device [nmodel*nstat] or NULL             */
+    int max_sweeps;             /* < 0: unlimited (debug)                    */
+} mceik_fsm_batch;
+
+/* Device workspace (bytes) a launch of this batch needs. */
+size_t mceik_fsm_workspace_bytes(const mceik_fsm_batch *b);
+/* Enqueue the batch on `stream` (hipStream_t; NULL = default).  No host
+ * synchronisation and no allocation: capturable in a hipGraph. 0 = ok. */
+int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes,
+                          void *stream);
+
+/* Algorithmic HBM bytes of one node visit in one sweep (roofline accounting). */
+double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b);
+
+/* Synchronous copy helper for hosts without a device runtime binding
+ * (kind: 0 host->device, 1 device->host, 2 device->device). 0 = ok. */
+int mceik_memcpy(void *dst, const void *src, size_t bytes, int kind);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

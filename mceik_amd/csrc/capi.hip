@@ -1,0 +1,598 @@
+// capi.hip -- C-ABI of libmceik_hip.so (include/mceik.h, include/mceik_eikonal.h).
+//
+// Host orchestration only: argument checks with the reference's error
+// behaviour, device allocation at init time, and kernel enqueueing.  The
+// numerics live in fsm_kernel.hip and mcmc_kernels.hip.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/mceik.h"
+#include "fsm_common.h"
+#include "mcmc_common.h"
+
+hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st);
+int fsm_occupancy(int is_double, int slow_mode, size_t lds);
+hipError_t fsm_to_brick_f64(const double *src, void *dst, int dst_double, const FsmLaunch &L, int nfield, hipStream_t st);
+hipError_t fsm_from_brick_f64(const void *src, int src_double, double *dst, const FsmLaunch &L, int nfield, hipStream_t st);
+hipError_t fsm_from_brick_f32(const float *src, float *dst, const FsmLaunch &L, int nfield, hipStream_t st);
+hipError_t fsm_to_brick_f32(const float *src, float *dst, const FsmLaunch &L, int nfield, hipStream_t st);
+hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st);
+hipError_t mcmc_init_loglik(const McmcDev &D, hipStream_t st);
+hipError_t mcmc_accept(const McmcDev &D, int keep_slot, hipStream_t st);
+hipError_t l2_gridsearch(int ldgrd, int ngrd, int nuse, int iwantOT, double t0use, const int *use,
+                         const double *tc, const double *wt, double xnorm, const double *test,
+                         double *t0, double *objfn, hipStream_t st);
+
+#define HIPCHK(x)                                                                      \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            fprintf(stderr, "mceik_hip: %s failed: %s (%s:%d)\n", #x,                  \
+                    hipGetErrorString(e_), __FILE__, __LINE__);                        \
+            return -1;                                                                 \
+        }                                                                              \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Convergence threshold T: the smallest power of two with
+// spacing(T^-) = T * 2^-p >= tol, p = 24 (fp32) or 53 (fp64).  A node whose
+// value was >= T when it changed has moved by >= tol, so only nodes below T
+// need their start-of-iteration value kept for the |u0 - u| < tol test.
+static double conv_threshold(double tol, int is_double)
+{
+    double tolr = is_double ? tol : (double)(float)tol;
+    if (!(tolr > 0.0)) return HUGE_VAL;
+    int p = is_double ? 53 : 24;
+    int k = (int)ceil(log2(tolr)) + p;
+    while (ldexp(1.0, k - p) < tolr) k++;
+    while (ldexp(1.0, k - 1 - p) >= tolr) k--;
+    double T = ldexp(1.0, k);
+    double big = is_double ? DBL_MAX : (double)FLT_MAX;
+    return T > big ? HUGE_VAL : T;
+}
+
+static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
+{
+    memset(&L, 0, sizeof(L));
+    L.nx = b->nx; L.ny = b->ny; L.nz = b->nz;
+    fsm_geometry(&L);
+    L.maxit = b->maxit; L.max_sweeps = b->max_sweeps;
+    L.tol = b->tol; L.h = b->h; L.x0 = b->x0; L.y0 = b->y0; L.z0 = b->z0;
+    int is_double = b->precision == 64;
+    double T = conv_threshold(b->tol, is_double);
+    L.conv_thresh = is_double ? (T == HUGE_VAL ? DBL_MAX : T) : (T == HUGE_VAL ? (double)FLT_MAX : T);
+    L.nsolve = b->nmodel * b->nstat; L.nstat = b->nstat; L.nsrc = b->nsrc;
+    L.src = b->src;
+    L.slow_mode = b->slow_mode;
+    L.nrx = b->nrx > 0 ? b->nrx : 1; L.nry = b->nry > 0 ? b->nry : 1; L.nrz = b->nrz > 0 ? b->nrz : 1;
+    L.ncx = mceik_div_up(L.nx, L.nrx); L.ncy = mceik_div_up(L.ny, L.nry); L.ncz = mceik_div_up(L.nz, L.nrz);
+    L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab;
+    L.niter = b->niter; L.ierr = b->ierr;
+}
+
+static int g_device_cus = 0;
+
+static int device_cus()
+{
+    if (g_device_cus == 0) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
+            g_device_cus = p.multiProcessorCount;
+        else
+            g_device_cus = 256;
+    }
+    return g_device_cus;
+}
+
+// Waves a launch keeps resident (one solve each): occupancy x CUs, at most nsolve.
+static int batch_waves(const FsmLaunch &L, int is_double)
+{
+    size_t lds = MCEIK_MAX_SRC * 6 * 4 + (size_t)L.nzb * 64 * (is_double ? 8 : 4);
+    int per_cu = fsm_occupancy(is_double, L.slow_mode, lds);
+    if (per_cu < 1) per_cu = 1;
+    long w = (long)per_cu * device_cus();
+    if (w > L.nsolve) w = L.nsolve;
+    return (int)(w < 1 ? 1 : w);
+}
+
+// Workspace: [counter 256 B][slow brick copy (mode 0)][u scratch][u0 scratch]
+struct WsLayout {
+    size_t counter, slow, u, u0, total;
+    int nwaves;
+};
+
+static WsLayout ws_layout(const mceik_fsm_batch *b)
+{
+    FsmLaunch L;
+    fill_launch(L, b);
+    int is_double = b->precision == 64;
+    size_t es = is_double ? 8 : 4;
+    WsLayout w;
+    w.nwaves = batch_waves(L, is_double);
+    w.counter = 0;
+    w.slow = 256;
+    size_t slow_bytes = b->slow_mode == 0 ? (size_t)b->nmodel * L.field_elems * es : 0;
+    w.u = w.slow + ((slow_bytes + 255) & ~(size_t)255);
+    size_t nu = b->u_out ? (size_t)L.nsolve : (size_t)w.nwaves;
+    w.u0 = w.u + nu * L.field_elems * es;
+    w.total = w.u0 + (size_t)w.nwaves * L.field_elems * es;
+    return w;
+}
+
+extern "C" size_t mceik_fsm_workspace_bytes(const mceik_fsm_batch *b)
+{
+    return ws_layout(b).total;
+}
+
+extern "C" double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b)
+{
+    // u read + u write per node visit; slowness read once per node per model
+    // pass, shared by the nstat stations of that model (SURVEY s.8d: N(8+4/S)).
+    double es = b->precision == 64 ? 8.0 : 4.0;
+    double s = b->slow_mode == 0 ? es : 4.0 / ((double)b->nrx * b->nry * b->nrz);
+    return 2.0 * es + s / (b->nstat > 0 ? b->nstat : 1);
+}
+
+extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes,
+                                     void *stream)
+{
+    if (!b || b->nx < 2 || b->ny < 2 || b->nz < 2 || b->nsrc < 1 || b->nsrc > MCEIK_MAX_SRC ||
+        b->nmodel < 1 || b->nstat < 1 || !(b->precision == 32 || b->precision == 64)) {
+        fprintf(stderr, "mceik_fsm_batch_solve: invalid batch description\n");
+        return 1;
+    }
+    if (b->slow_mode == 1 && b->precision != 32 && b->precision != 64) return 1;
+    WsLayout w = ws_layout(b);
+    if (!workspace || workspace_bytes < w.total) {
+        fprintf(stderr, "mceik_fsm_batch_solve: workspace too small (%zu < %zu)\n", workspace_bytes, w.total);
+        return 1;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    int is_double = b->precision == 64;
+    FsmLaunch L;
+    fill_launch(L, b);
+    char *ws = (char *)workspace;
+    L.counter = (unsigned *)(ws + w.counter);
+    HIPCHK(hipMemsetAsync(L.counter, 0, 256, st));
+    if (b->slow_mode == 0) {
+        void *sb = ws + w.slow;
+        if (is_double)
+            HIPCHK(fsm_to_brick_f64((const double *)b->slow, sb, 1, L, b->nmodel, st));
+        else
+            HIPCHK(fsm_to_brick_f32((const float *)b->slow, (float *)sb, L, b->nmodel, st));
+        L.slow = sb;
+    } else {
+        L.slow = b->slow;
+    }
+    L.u = ws + w.u;
+    L.u0 = ws + w.u0;
+    L.slot_per_solve = b->u_out ? 1 : 0;
+    HIPCHK(fsm_launch(L, is_double, w.nwaves, st));
+    if (b->u_out) {
+        if (is_double) HIPCHK(fsm_from_brick_f64(L.u, 1, (double *)b->u_out, L, L.nsolve, st));
+        else HIPCHK(fsm_from_brick_f32((const float *)L.u, (float *)b->u_out, L, L.nsolve, st));
+    }
+    return 0;
+}
+
+extern "C" int mceik_memcpy(void *dst, const void *src, size_t bytes, int kind)
+{
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIPCHK(hipMemcpy(dst, src, bytes, k));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in serial driver (fsm3d.f90:1968-2052).  The reference keeps a level
+// structure between job 1 and job 3 (SAVE lstruct, linit); the GPU schedule
+// needs none, so only the init flag is kept, with the same error behaviour.
+static int g_serial_init[2] = {0, 0};
+
+static void serial_driver(int is_double, const int *job, const int *iverb, const int *maxit,
+                          const int *nsrc, const int *nx, const int *ny, const int *nz,
+                          const double *tol, const double *h, const double *x0, const double *y0,
+                          const double *z0, const double *ts, const double *xs, const double *ys,
+                          const double *zs, const double *slow, double *u, int *ierr)
+{
+    int &linit = g_serial_init[is_double];
+    *ierr = 0;
+    if (*job == 1) {
+        if (linit) { printf(" eikonal3d_serial_driver: Already initialized!\n"); *ierr = 1; return; }
+        if (*iverb > 0) printf(" eikonal3d_serial_driver: Generating levels...\n");
+        linit = 1;
+        return;
+    }
+    if (*job != 2) {
+        if (!linit) printf(" eikonal3d_serial_driver: Never initialized!\n");
+        linit = 0;
+        return;
+    }
+    if (!linit) { printf(" eikonal3d_serial_driver: Solver not initalized!\n"); *ierr = 1; return; }
+    if (*nsrc < 1 || *nsrc > MCEIK_MAX_SRC) {
+        printf(" eikonal3d_serial_driver: nsrc must be in [1,%d]\n", MCEIK_MAX_SRC);
+        *ierr = 1;
+        return;
+    }
+    size_t n = (size_t)(*nx) * (*ny) * (*nz);
+    std::vector<double> src((size_t)(*nsrc) * 4);
+    for (int s = 0; s < *nsrc; s++) {
+        src[s * 4 + 0] = ts[s]; src[s * 4 + 1] = xs[s]; src[s * 4 + 2] = ys[s]; src[s * 4 + 3] = zs[s];
+    }
+    mceik_fsm_batch b;
+    memset(&b, 0, sizeof(b));
+    b.nx = *nx; b.ny = *ny; b.nz = *nz; b.h = *h; b.x0 = *x0; b.y0 = *y0; b.z0 = *z0;
+    b.maxit = *maxit; b.tol = *tol; b.precision = is_double ? 64 : 32;
+    b.nmodel = 1; b.nstat = 1; b.nsrc = *nsrc; b.slow_mode = 0; b.max_sweeps = -1;
+    size_t es = is_double ? 8 : 4;
+    void *d_slow = nullptr, *d_u = nullptr, *ws = nullptr;
+    double *d_src = nullptr;
+    int *d_ierr = nullptr;
+    hipError_t e = hipSuccess;
+    size_t wsb;
+    std::vector<float> h32;
+    auto fail = [&](const char *what) {
+        printf(" eikonal3d_serial_driver: %s failed (%s)\n", what, hipGetErrorString(e));
+        *ierr = 1;
+    };
+    if ((e = hipMalloc(&d_slow, n * es)) != hipSuccess) { fail("hipMalloc"); goto done; }
+    if ((e = hipMalloc(&d_u, n * es)) != hipSuccess) { fail("hipMalloc"); goto done; }
+    if ((e = hipMalloc(&d_src, src.size() * 8)) != hipSuccess) { fail("hipMalloc"); goto done; }
+    if ((e = hipMalloc(&d_ierr, sizeof(int))) != hipSuccess) { fail("hipMalloc"); goto done; }
+    if (is_double) {
+        e = hipMemcpy(d_slow, slow, n * 8, hipMemcpyHostToDevice);
+    } else {
+        h32.resize(n);
+        for (size_t i = 0; i < n; i++) h32[i] = (float)slow[i];
+        e = hipMemcpy(d_slow, h32.data(), n * 4, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) { fail("hipMemcpy"); goto done; }
+    if ((e = hipMemcpy(d_src, src.data(), src.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) { fail("hipMemcpy"); goto done; }
+    b.src = d_src; b.slow = d_slow; b.u_out = d_u; b.ierr = d_ierr;
+    wsb = mceik_fsm_workspace_bytes(&b);
+    if ((e = hipMalloc(&ws, wsb)) != hipSuccess) { fail("hipMalloc"); goto done; }
+    if (*iverb > 0) printf(" eikonal3d_serial_driver: Solving...\n");
+    if (mceik_fsm_batch_solve(&b, ws, wsb, nullptr) != 0) { *ierr = 1; goto done; }
+    if ((e = hipDeviceSynchronize()) != hipSuccess) { fail("solve"); goto done; }
+    if (is_double) {
+        e = hipMemcpy(u, d_u, n * 8, hipMemcpyDeviceToHost);
+    } else {
+        h32.resize(n);
+        e = hipMemcpy(h32.data(), d_u, n * 4, hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < n && e == hipSuccess; i++) u[i] = (double)h32[i];
+    }
+    if (e != hipSuccess) { fail("hipMemcpy"); goto done; }
+    if ((e = hipMemcpy(ierr, d_ierr, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess) { fail("hipMemcpy"); goto done; }
+    if (*ierr != 0) {
+        if (*ierr == 1 && 0) {}
+        printf(" eikonal3d_serial_driver: Error solving eikonal equation\n");
+    }
+done:
+    hipFree(d_slow); hipFree(d_u); hipFree(d_src); hipFree(d_ierr); hipFree(ws);
+}
+
+extern "C" void eikonal3d_serial_driver(const int *job, const int *iverb, const int *maxit, const int *nsrc,
+                                        const int *nx, const int *ny, const int *nz, const double *tol,
+                                        const double *h, const double *x0, const double *y0, const double *z0,
+                                        const double *ts, const double *xs, const double *ys, const double *zs,
+                                        const double *slow, double *u, int *ierr)
+{
+    serial_driver(1, job, iverb, maxit, nsrc, nx, ny, nz, tol, h, x0, y0, z0, ts, xs, ys, zs, slow, u, ierr);
+}
+
+extern "C" void eikonal3d_serial_driver_sp(const int *job, const int *iverb, const int *maxit, const int *nsrc,
+                                           const int *nx, const int *ny, const int *nz, const double *tol,
+                                           const double *h, const double *x0, const double *y0, const double *z0,
+                                           const double *ts, const double *xs, const double *ys, const double *zs,
+                                           const double *slow, double *u, int *ierr)
+{
+    serial_driver(0, job, iverb, maxit, nsrc, nx, ny, nz, tol, h, x0, y0, z0, ts, xs, ys, zs, slow, u, ierr);
+}
+
+// ---------------------------------------------------------------------------
+// locate_l2_gridSearch__double64 drop-in (locate.c:923-1047).
+extern "C" int locate_l2_gridSearch__double64(int ldgrd, int ngrd, int nobs, int iwantOT, double t0use,
+                                              const int *mask, const double *tobs, const double *tcorr,
+                                              const double *varobs, const double *test,
+                                              double *t0, double *objfn)
+{
+    const char *fcnm = "locate_l2_gridSearch__double64";
+    if ((sizeof(double) * (size_t)ldgrd) % 64 != 0 || ldgrd < ngrd || nobs < 1 || !mask || !tobs ||
+        !varobs || !test || !t0 || !objfn) {
+        if ((sizeof(double) * (size_t)ldgrd) % 64 != 0) printf("%s: Error ldgrd must be divisible by 64\n", fcnm);
+        if (ldgrd < ngrd) printf("%s: Error ldgrd < ngrd\n", fcnm);
+        if (!mask) printf("%s: mask is null\n", fcnm);
+        if (!tobs) printf("%s: tobs is null\n", fcnm);
+        if (!varobs) printf("%s: varobs is null\n", fcnm);
+        if (!test) printf("%s: test is null\n", fcnm);
+        if (!t0) printf("%s: t0 is null\n", fcnm);
+        if (!objfn) printf("%s: objfn is null\n", fcnm);
+        return 1;
+    }
+    if (((uintptr_t)t0 % 64) || ((uintptr_t)test % 64) || ((uintptr_t)objfn % 64)) {
+        printf("%s: Input arrays are not 64 bit aligned\n", fcnm);
+        return 1;
+    }
+    std::vector<int> use;
+    std::vector<double> tc, wt;
+    double xnorm = 0.0;
+    for (int i = 0; i < nobs; i++) {
+        if (mask[i] != 0) continue;
+        tc.push_back(tcorr ? tobs[i] - tcorr[i] : tobs[i]);
+        use.push_back(i);
+        wt.push_back(1.0 / varobs[i]);
+        xnorm = xnorm + wt.back();
+    }
+    int nuse = (int)use.size();
+    int *d_use = nullptr;
+    double *d_tc = nullptr, *d_wt = nullptr, *d_test = nullptr, *d_t0 = nullptr, *d_obj = nullptr;
+    int rc = 1;
+    size_t tb = (size_t)ldgrd * nobs * 8;
+    if (hipMalloc(&d_use, (nuse + 1) * 4) != hipSuccess || hipMalloc(&d_tc, (nuse + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_wt, (nuse + 1) * 8) != hipSuccess || hipMalloc(&d_test, tb) != hipSuccess ||
+        hipMalloc(&d_t0, (size_t)ngrd * 8 + 8) != hipSuccess || hipMalloc(&d_obj, (size_t)ngrd * 8 + 8) != hipSuccess)
+        goto out;
+    if (nuse) {
+        hipMemcpy(d_use, use.data(), nuse * 4, hipMemcpyHostToDevice);
+        hipMemcpy(d_tc, tc.data(), nuse * 8, hipMemcpyHostToDevice);
+        hipMemcpy(d_wt, wt.data(), nuse * 8, hipMemcpyHostToDevice);
+    }
+    hipMemcpy(d_test, test, tb, hipMemcpyHostToDevice);
+    if (l2_gridsearch(ldgrd, ngrd, nuse, iwantOT, t0use, d_use, d_tc, d_wt, xnorm, d_test, d_t0, d_obj, nullptr) != hipSuccess)
+        goto out;
+    if (hipMemcpy(t0, d_t0, (size_t)ngrd * 8, hipMemcpyDeviceToHost) != hipSuccess) goto out;
+    if (hipMemcpy(objfn, d_obj, (size_t)ngrd * 8, hipMemcpyDeviceToHost) != hipSuccess) goto out;
+    rc = 0;
+out:
+    hipFree(d_use); hipFree(d_tc); hipFree(d_wt); hipFree(d_test); hipFree(d_t0); hipFree(d_obj);
+    if (rc) printf("%s: device failure\n", fcnm);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// MCMC sampler (include/mceik.h)
+struct mceik_mcmc {
+    McmcDev D;
+    mceik_fsm_batch fb;
+    int device, max_samples, nburn, keepk, nkept;
+    long long step;
+    hipStream_t stream;
+    void *ws;
+    size_t ws_bytes;
+    std::vector<void *> allocs;
+};
+
+template <typename T>
+static int dalloc(mceik_mcmc *s, T **p, size_t count)
+{
+    void *q = nullptr;
+    if (hipMalloc(&q, count * sizeof(T) + 16) != hipSuccess) return -1;
+    hipMemset(q, 0, count * sizeof(T) + 16);
+    s->allocs.push_back(q);
+    *p = (T *)q;
+    return 0;
+}
+
+template <typename T>
+static int dput(mceik_mcmc *s, T **p, const T *host, size_t count)
+{
+    if (dalloc(s, p, count)) return -1;
+    if (count && hipMemcpy(*p, host, count * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) return -1;
+    return 0;
+}
+
+static int source_index(int n, double x0, double dx, double xs)   // fsm3d.f90:697-711 (0-based)
+{
+    if (xs <= x0) return 0;
+    if (xs >= x0 + (double)(n - 1) * dx) return n - 1;
+    return (int)((xs - x0) / dx + 0.5);
+}
+
+static int mcmc_forward(mceik_mcmc *s)
+{
+    if (mceik_fsm_batch_solve(&s->fb, s->ws, s->ws_bytes, s->stream)) return -1;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const struct mceik_stations_struct *st,
+                               const struct mceik_catalog_struct *cat, const mceik_mcmc_opts *o,
+                               const int *v0, mceik_mcmc **out)
+{
+    if (!parms || !st || !cat || !o || !v0 || !out) return 1;
+    *out = nullptr;
+    if (parms->dx != parms->dy || parms->dx != parms->dz || parms->dx <= 0.0) {
+        fprintf(stderr, "mceik_mcmc_init: the eikonal solver needs dx = dy = dz\n");
+        return 1;
+    }
+    if (o->nx < 2 || o->ny < 2 || o->nz < 2 || o->nchains < 1 || st->nstat < 1 || cat->nevents < 1 ||
+        o->vmin < 1 || o->vmax < o->vmin || o->dvmax < 1) {
+        fprintf(stderr, "mceik_mcmc_init: invalid options\n");
+        return 1;
+    }
+    if (hipSetDevice(o->device) != hipSuccess) return -1;
+    mceik_mcmc *s = new mceik_mcmc();
+    s->device = o->device;
+    s->stream = nullptr;
+    s->step = 0;
+    s->nkept = 0;
+    s->nburn = parms->mcparms.nburnIn;
+    s->keepk = parms->mcparms.keepK > 0 ? parms->mcparms.keepK : 1;
+    s->max_samples = o->max_samples > 0 ? o->max_samples : 0;
+    int nrx = parms->nrefx > 0 ? parms->nrefx : 1, nry = parms->nrefy > 0 ? parms->nrefy : 1,
+        nrz = parms->nrefz > 0 ? parms->nrefz : 1;
+    int ncx = mceik_div_up(o->nx, nrx), ncy = mceik_div_up(o->ny, nry), ncz = mceik_div_up(o->nz, nrz);
+    int ncell = ncx * ncy * ncz;
+    int nstat = st->nstat, nev = cat->nevents, nch = o->nchains;
+    McmcDev &D = s->D;
+    memset(&D, 0, sizeof(D));
+    D.nchains = nch; D.chain_offset = o->chain_offset; D.ncell = ncell; D.nstat = nstat; D.nev = nev;
+    D.vmin = o->vmin; D.vmax = o->vmax; D.dvmax = o->dvmax; D.seed = o->seed;
+    // host-side problem tables
+    std::vector<double> src((size_t)nstat * 4);
+    for (int i = 0; i < nstat; i++) {
+        src[i * 4 + 0] = 0.0; src[i * 4 + 1] = st->xrec[i]; src[i * 4 + 2] = st->yrec[i]; src[i * 4 + 3] = st->zrec[i];
+    }
+    std::vector<int> ev(nev);
+    for (int e = 0; e < nev; e++) {
+        int ix = source_index(o->nx, parms->x0, parms->dx, cat->xsrc[e]);
+        int iy = source_index(o->ny, parms->y0, parms->dx, cat->ysrc[e]);
+        int iz = source_index(o->nz, parms->z0, parms->dx, cat->zsrc[e]);
+        ev[e] = (iz * o->ny + iy) * o->nx + ix;
+    }
+    int nobs = cat->obsPtr[nev];
+    std::vector<int> ostat(nobs > 0 ? nobs : 1), omask(nobs > 0 ? nobs : 1);
+    std::vector<double> tcorr(nobs > 0 ? nobs : 1);
+    for (int j = 0; j < nobs; j++) {
+        int k = cat->statPtr[j] - 1;
+        int use = cat->luseObs[j] != 0 && cat->pickType[j] == P_PRIMARY_PICK && k >= 0 && k < nstat;
+        ostat[j] = use ? k : 0;
+        omask[j] = !use;
+        tcorr[j] = (use && st->pcorr) ? st->pcorr[k] : 0.0;
+    }
+    std::vector<float> sl((size_t)nch * ncell);
+    for (size_t i = 0; i < sl.size(); i++) sl[i] = 1.0f / (float)v0[i];
+    int rc = 0;
+    double *d_src = nullptr;
+    int *d_ev = nullptr, *d_optr = nullptr;
+    float *d_tt = nullptr;
+    int *d_niter = nullptr, *d_ierr = nullptr;
+    rc |= dput(s, &d_src, src.data(), src.size());
+    rc |= dput(s, &d_ev, ev.data(), ev.size());
+    rc |= dput(s, &d_optr, (const int *)cat->obsPtr, (size_t)nev + 1);
+    int *d_ostat = nullptr, *d_omask = nullptr;
+    double *d_tobs = nullptr, *d_tcorr = nullptr, *d_var = nullptr;
+    rc |= dput(s, &d_ostat, ostat.data(), ostat.size());
+    rc |= dput(s, &d_omask, omask.data(), omask.size());
+    rc |= dput(s, &d_tobs, (const double *)cat->tobs, (size_t)(nobs > 0 ? nobs : 0));
+    rc |= dput(s, &d_tcorr, tcorr.data(), tcorr.size());
+    rc |= dput(s, &d_var, (const double *)cat->varObs, (size_t)(nobs > 0 ? nobs : 0));
+    rc |= dput(s, &D.v, v0, (size_t)nch * ncell);
+    rc |= dput(s, &D.slow_cur, sl.data(), sl.size());
+    rc |= dput(s, &D.slow_prop, sl.data(), sl.size());
+    rc |= dalloc(s, &D.logl, nch);
+    rc |= dalloc(s, &D.naccept, nch);
+    rc |= dalloc(s, &D.prop_cell, nch);
+    rc |= dalloc(s, &D.prop_v, nch);
+    rc |= dalloc(s, &D.prop_inprior, nch);
+    rc |= dalloc(s, &D.prop_logu, nch);
+    rc |= dalloc(s, &D.accept, nch);
+    rc |= dalloc(s, &d_tt, (size_t)nch * nstat * nev);
+    rc |= dalloc(s, &d_niter, (size_t)nch * nstat);
+    rc |= dalloc(s, &d_ierr, (size_t)nch * nstat);
+    if (s->max_samples) {
+        rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncell);
+        rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
+    }
+    if (rc) { mceik_mcmc_finalize(&s); return -1; }
+    D.ttab = d_tt; D.obs_ptr = d_optr; D.obs_stat = d_ostat; D.obs_mask = d_omask;
+    D.tobs = d_tobs; D.tcorr = d_tcorr; D.var = d_var;
+    mceik_fsm_batch &b = s->fb;
+    memset(&b, 0, sizeof(b));
+    b.nx = o->nx; b.ny = o->ny; b.nz = o->nz; b.h = parms->dx;
+    b.x0 = parms->x0; b.y0 = parms->y0; b.z0 = parms->z0;
+    b.maxit = parms->eikparms.maxit; b.tol = parms->eikparms.tol; b.precision = 32;
+    b.nmodel = nch; b.nstat = nstat; b.nsrc = 1; b.src = d_src;
+    b.slow_mode = 1; b.slow = D.slow_prop; b.nrx = nrx; b.nry = nry; b.nrz = nrz;
+    b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = d_ierr;
+    b.max_sweeps = -1;
+    s->ws_bytes = mceik_fsm_workspace_bytes(&b);
+    if (hipMalloc(&s->ws, s->ws_bytes) != hipSuccess) {
+        fprintf(stderr, "mceik_mcmc_init: cannot allocate %zu B of FSM workspace\n", s->ws_bytes);
+        mceik_mcmc_finalize(&s);
+        return -1;
+    }
+    // initial log-likelihood of every chain
+    if (mcmc_forward(s) || mcmc_init_loglik(D, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
+        mceik_mcmc_finalize(&s);
+        return -1;
+    }
+    *out = s;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_set_stream(mceik_mcmc *s, void *stream)
+{
+    if (!s) return 1;
+    s->stream = (hipStream_t)stream;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
+{
+    if (!s || nsteps < 0) return 1;
+    for (int i = 0; i < nsteps; i++) {
+        uint64_t step = (uint64_t)s->step;
+        HIPCHK(mcmc_propose(s->D, step, s->stream));
+        if (mcmc_forward(s)) return -1;
+        int slot = -1;
+        if (s->max_samples && s->step >= s->nburn && (s->step - s->nburn) % s->keepk == 0) {
+            slot = s->nkept % s->max_samples;
+            s->nkept++;
+        }
+        HIPCHK(mcmc_accept(s->D, slot, s->stream));
+        s->step++;
+    }
+    return 0;
+}
+
+extern "C" int mceik_mcmc_sync(mceik_mcmc *s)
+{
+    if (!s) return 1;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return 0;
+}
+
+extern "C" int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long long *naccept, long long *step)
+{
+    if (!s) return 1;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    const McmcDev &D = s->D;
+    if (v) HIPCHK(hipMemcpy(v, D.v, (size_t)D.nchains * D.ncell * 4, hipMemcpyDeviceToHost));
+    if (logl) HIPCHK(hipMemcpy(logl, D.logl, (size_t)D.nchains * 8, hipMemcpyDeviceToHost));
+    if (naccept) HIPCHK(hipMemcpy(naccept, D.naccept, (size_t)D.nchains * 8, hipMemcpyDeviceToHost));
+    if (step) *step = s->step;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max, int kind, int *nkept)
+{
+    if (!s) return 1;
+    int have = s->nkept < s->max_samples ? s->nkept : s->max_samples;
+    int n = have < max ? have : max;
+    if (nkept) *nkept = n;
+    if (n <= 0) return 0;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    hipMemcpyKind k = kind ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    size_t per = (size_t)s->D.nchains * s->D.ncell;
+    if (v_out) HIPCHK(hipMemcpy(v_out, s->D.keep_v, (size_t)n * per * 4, k));
+    if (logl_out) HIPCHK(hipMemcpy(logl_out, s->D.keep_logl, (size_t)n * s->D.nchains * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept)
+{
+    if (!s) return 1;
+    if (ttab) *ttab = s->fb.ttab;
+    if (niter) *niter = s->fb.niter;
+    if (accept) *accept = s->D.accept;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
+{
+    if (!ps || !*ps) return 0;
+    mceik_mcmc *s = *ps;
+    hipStreamSynchronize(s->stream);
+    for (void *p : s->allocs) hipFree(p);
+    if (s->ws) hipFree(s->ws);
+    delete s;
+    *ps = nullptr;
+    return 0;
+}

@@ -1,0 +1,48 @@
+// fsm_common.h -- shared host/device definitions for the batched fast-sweeping
+// eikonal solve (MI355X / gfx950).  Not a public header: the C-ABI lives in
+// include/mceik_eikonal.h and include/mceik.h.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#define MCEIK_MAX_SRC 8          // point sources per solve (box BCs, fsm3d.f90:762-840)
+#define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
+#define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
+#define MCEIK_MIN_SB 11          // virtual bricks per tile (>= nzb); halo lags need >= 11
+
+// One batched launch: nsolve = nmodel * nstat solves; solve id = model*nstat + station.
+struct FsmLaunch {
+    int nx, ny, nz;              // eikonal grid (nodes); dx = dy = dz = h
+    int ntx, nty, nzb, sb, ntiles;
+    int maxit, max_sweeps;       // max_sweeps < 0: unlimited (debug bisection aid)
+    double tol, h, x0, y0, z0;
+    double conv_thresh;          // T: nodes >= T converge iff unchanged
+    int nsolve, nstat, nsrc;     // sources of station s: src[(s*nsrc + k)*4 + {0:ts,1:xs,2:ys,3:zs}]
+    const double *src;
+    int slow_mode;               // 0: per-node field (brick layout, R); 1: inversion grid (float)
+    const void *slow;            // mode 0: [nmodel][field_elems] R ; mode 1: [nmodel][ncell] float
+    int ncx, ncy, ncz, nrx, nry, nrz;
+    size_t field_elems;          // ntiles * nzb * 512
+    void *u;                     // travel-time fields (brick layout, R)
+    void *u0;                    // convergence side field (same layout)
+    int slot_per_solve;          // 1: field slot = solve id; 0: slot = blockIdx.x (scratch)
+    const int *ev_node;          // event nodes (x-fastest linear index), may be null
+    int nev;
+    float *ttab;                 // [nsolve][nev] travel times at events (fp32), may be null
+    int *niter;                  // [nsolve] iterations executed, may be null
+    int *ierr;                   // [nsolve] reference ierr semantics, may be null
+    unsigned *counter;           // work queue head (zeroed before the launch)
+};
+
+static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
+
+// Fills the tile geometry of a launch from nx, ny, nz.
+static inline void fsm_geometry(FsmLaunch *L)
+{
+    L->ntx = mceik_div_up(L->nx, MCEIK_TILE);
+    L->nty = mceik_div_up(L->ny, MCEIK_TILE);
+    L->nzb = mceik_div_up(L->nz, MCEIK_TILE);
+    L->sb = L->nzb > MCEIK_MIN_SB ? L->nzb : MCEIK_MIN_SB;
+    L->ntiles = L->ntx * L->nty;
+    L->field_elems = (size_t)L->ntiles * L->nzb * MCEIK_BRICK;
+}

@@ -1,0 +1,22 @@
+// mcmc_common.h -- device-side state of the per-GPU sampler (not public).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+struct McmcDev {
+    int nchains, chain_offset, ncell, nstat, nev;
+    int vmin, vmax, dvmax;
+    uint32_t seed;
+    int *v;                        // [nchains][ncell] current model (m/s)
+    float *slow_cur, *slow_prop;   // [nchains][ncell] 1/v of current / proposed
+    double *logl;                  // [nchains]
+    long long *naccept;            // [nchains]
+    int *prop_cell, *prop_v, *prop_inprior;
+    double *prop_logu;
+    unsigned char *accept;         // [nchains] last step
+    const float *ttab;             // [nchains][nstat][nev]
+    const int *obs_ptr, *obs_stat, *obs_mask;
+    const double *tobs, *tcorr, *var;
+    int *keep_v;                   // [max_samples][nchains][ncell]
+    double *keep_logl;             // [max_samples][nchains]
+};

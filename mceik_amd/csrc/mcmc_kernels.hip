@@ -1,0 +1,194 @@
+// mcmc_kernels.hip -- proposal, L2 misfit + Metropolis, and the L2 grid
+// search, on gfx950.
+//
+// The reference defines no MCMC (include/mceik.h:1-14 is empty; only
+// mcmc_parms_struct, mceik_struct.h:54-60).  The definition used here
+//  is restated on the CPU in oracle/mceik_oracle.c and the two
+// agree bit for bit: integer Philox4x32-10 draws, a log built from IEEE
+// +,-,*,/ only, and an fp64 misfit summed in observation order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mcmc_common.h"
+
+namespace {
+
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1; c[3] = (uint32_t)p0; c[0] = n0; c[2] = n2;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+
+// Natural log from IEEE basic operations only (host twin: oracle_det_log).
+__device__ __forceinline__ double det_log(double x)
+{
+    uint64_t b = __double_as_longlong(x);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    double m = __longlong_as_double((long long)((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
+    double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double p = 1.0 / 25.0;
+    p = p * s2 + 1.0 / 23.0; p = p * s2 + 1.0 / 21.0; p = p * s2 + 1.0 / 19.0;
+    p = p * s2 + 1.0 / 17.0; p = p * s2 + 1.0 / 15.0; p = p * s2 + 1.0 / 13.0;
+    p = p * s2 + 1.0 / 11.0; p = p * s2 + 1.0 / 9.0;  p = p * s2 + 1.0 / 7.0;
+    p = p * s2 + 1.0 / 5.0;  p = p * s2 + 1.0 / 3.0;  p = p * s2 + 1.0;
+    double de = (double)e;
+    return de * 6.93147180369123816490e-01 + (2.0 * s * p + de * 1.90821492927058770002e-10);
+}
+
+// One proposal per chain: a single inversion cell moves by +-[1, dvmax] m/s.
+// slow_prop (== slow_cur everywhere but the proposed cell) gets the new cell.
+__global__ void propose_kernel(McmcDev D, uint64_t step)
+{
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= D.nchains) return;
+    uint32_t ctr[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0u, 0u};
+    philox4x32_10(ctr, (uint32_t)(D.chain_offset + c), D.seed);
+    int cell = (int)(((uint64_t)ctr[0] * (uint32_t)D.ncell) >> 32);
+    int mag = 1 + (int)(((uint64_t)ctr[1] * (uint32_t)D.dvmax) >> 32);
+    int vold = D.v[(size_t)c * D.ncell + cell];
+    int vn = vold + ((ctr[2] & 1u) ? -mag : mag);
+    int inp = vn >= D.vmin && vn <= D.vmax;
+    D.prop_cell[c] = cell;
+    D.prop_v[c] = vn;
+    D.prop_inprior[c] = inp;
+    D.prop_logu[c] = det_log(((double)ctr[3] + 0.5) * (1.0 / 4294967296.0));
+    if (inp) D.slow_prop[(size_t)c * D.ncell + cell] = 1.0f / (float)vn;
+}
+
+// logL = -sum_e objfn_e, objfn_e the L2 misfit with analytic origin time
+// (locate.c:923-1047 at one grid point, iwantOT = 1), observations in CSR order.
+__device__ double chain_loglik(const McmcDev &D, int c)
+{
+    const float *tt = D.ttab + (size_t)c * D.nstat * D.nev;
+    const double sqrt2i = 0.7071067811865475;
+    double logl = 0.0;
+    for (int e = 0; e < D.nev; e++) {
+        int j0 = D.obs_ptr[e], j1 = D.obs_ptr[e + 1];
+        double xnorm = 0.0, t0 = 0.0, obj = 0.0;
+        for (int j = j0; j < j1; j++) if (!D.obs_mask[j]) xnorm = xnorm + 1.0 / D.var[j];
+        for (int j = j0; j < j1; j++) {
+            if (D.obs_mask[j]) continue;
+            double te = (double)tt[(size_t)D.obs_stat[j] * D.nev + e];
+            double tc = D.tobs[j] - D.tcorr[j];
+            t0 = t0 + ((1.0 / D.var[j]) / xnorm) * (tc - te);
+        }
+        for (int j = j0; j < j1; j++) {
+            if (D.obs_mask[j]) continue;
+            double te = (double)tt[(size_t)D.obs_stat[j] * D.nev + e];
+            double tc = D.tobs[j] - D.tcorr[j];
+            double res = ((1.0 / D.var[j]) * sqrt2i) * (tc - (te + t0));
+            obj = obj + res * res;
+        }
+        logl = logl - obj;
+    }
+    return logl;
+}
+
+__global__ void init_loglik_kernel(McmcDev D)
+{
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= D.nchains) return;
+    D.logl[c] = chain_loglik(D, c);
+}
+
+// Metropolis accept/reject; keeps slow_cur/slow_prop identical except while a
+// proposal is pending, so each step touches one cell per chain.
+__global__ void accept_kernel(McmcDev D, int keep_slot)
+{
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= D.nchains) return;
+    int cell = D.prop_cell[c];
+    size_t ci = (size_t)c * D.ncell + cell;
+    int acc = 0;
+    if (D.prop_inprior[c]) {
+        double ln = chain_loglik(D, c);
+        acc = D.prop_logu[c] < ln - D.logl[c];
+        if (acc) {
+            D.logl[c] = ln;
+            D.v[ci] = D.prop_v[c];
+            D.slow_cur[ci] = D.slow_prop[ci];
+            D.naccept[c] += 1;
+        } else {
+            D.slow_prop[ci] = D.slow_cur[ci];
+        }
+    }
+    D.accept[c] = (unsigned char)acc;
+    if (keep_slot >= 0) D.keep_logl[(size_t)keep_slot * D.nchains + c] = D.logl[c];
+}
+
+// Kept state copy: [slot][chain][cell] int (after accept_kernel).
+__global__ void keep_kernel(McmcDev D, int keep_slot)
+{
+    size_t n = (size_t)D.nchains * D.ncell;
+    int *dst = D.keep_v + (size_t)keep_slot * n;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = D.v[i];
+}
+
+// ---- L2 grid search (locate.c:923-1047) over all grid points -----------------
+// obs already compacted on the host in the reference's order: use[j] (row of
+// test), tc[j] = tobs - tcorr, wt[j] = 1/var; xnorm = sum wt (host, same order).
+__global__ void l2_gridsearch_kernel(int ldgrd, int ngrd, int nuse, int iwantOT, double t0use,
+                                     const int *use, const double *tc, const double *wt, double xnorm,
+                                     const double *test, double *t0, double *objfn)
+{
+    const double sqrt2i = 0.7071067811865475;
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < ngrd; g += gridDim.x * blockDim.x) {
+        double t = 0.0;
+        if (iwantOT == 1) {
+            for (int j = 0; j < nuse; j++) {
+                double w = wt[j] / xnorm;
+                t = t + w * (tc[j] - test[(size_t)ldgrd * use[j] + g]);
+            }
+        } else {
+            t = t0use;
+        }
+        double o = 0.0;
+        for (int j = 0; j < nuse; j++) {
+            double w = wt[j] * sqrt2i;
+            double res = w * (tc[j] - (test[(size_t)ldgrd * use[j] + g] + t));
+            o = o + res * res;
+        }
+        t0[g] = t;
+        objfn[g] = o;
+    }
+}
+
+}  // namespace
+
+hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st)
+{
+    hipLaunchKernelGGL(propose_kernel, dim3((D.nchains + 255) / 256), dim3(256), 0, st, D, step);
+    return hipGetLastError();
+}
+
+hipError_t mcmc_init_loglik(const McmcDev &D, hipStream_t st)
+{
+    hipLaunchKernelGGL(init_loglik_kernel, dim3((D.nchains + 63) / 64), dim3(64), 0, st, D);
+    return hipGetLastError();
+}
+
+hipError_t mcmc_accept(const McmcDev &D, int keep_slot, hipStream_t st)
+{
+    hipLaunchKernelGGL(accept_kernel, dim3((D.nchains + 63) / 64), dim3(64), 0, st, D, keep_slot);
+    if (keep_slot >= 0)
+        hipLaunchKernelGGL(keep_kernel, dim3(512), dim3(256), 0, st, D, keep_slot);
+    return hipGetLastError();
+}
+
+hipError_t l2_gridsearch(int ldgrd, int ngrd, int nuse, int iwantOT, double t0use, const int *use,
+                         const double *tc, const double *wt, double xnorm, const double *test,
+                         double *t0, double *objfn, hipStream_t st)
+{
+    int blocks = (ngrd + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(l2_gridsearch_kernel, dim3(blocks), dim3(256), 0, st, ldgrd, ngrd, nuse, iwantOT,
+                       t0use, use, tc, wt, xnorm, test, t0, objfn);
+    return hipGetLastError();
+}

@@ -1,0 +1,145 @@
+"""Host mirror of the reference's eikonal entry points, computed by libmceik_hip.so.
+
+`eikonal3d_serial_driver` keeps the reference's calling convention
+(fsm3d.f90:1968-2052: job 1 init / 2 solve / other free, ierr out, caller-owned
+fp64 arrays x fastest).  `batch_solve` is the batched GPU path on torch device
+tensors (one launch, nmodel x nstat solves).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+
+
+def _ip(v):
+    return C.byref(C.c_int(int(v)))
+
+
+def _dp(v):
+    return C.byref(C.c_double(float(v)))
+
+
+def _arr(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(C.c_void_p)
+
+
+def eikonal3d_serial_driver(job, iverb, maxit, nsrc, nx, ny, nz, tol, h, x0, y0, z0,
+                            ts, xs, ys, zs, slow, u, precision=64):
+    """Same arguments and ierr behaviour as the reference; fills `u` in place.
+
+    precision=64: bitwise the reference.  precision=32: fp32 GPU path within
+    the stated tolerance (|du| <= 1e-6 u + 1e-7 s).
+    """
+    L = _lib.lib()
+    f = L.eikonal3d_serial_driver if precision == 64 else L.eikonal3d_serial_driver_sp
+    n = int(nx) * int(ny) * int(nz)
+    keep = [_arr(np.atleast_1d(v)) for v in (ts, xs, ys, zs)]
+    if job == 2:
+        slow_a, slow_p = _arr(slow)
+        if slow_a.size < n or u.size < n or u.dtype != np.float64 or not u.flags.c_contiguous:
+            raise ValueError("slow/u must hold nx*ny*nz float64 values (u C-contiguous)")
+        u_p = u.ctypes.data_as(C.c_void_p)
+    else:
+        slow_a, slow_p, u_p = None, None, None
+    ierr = C.c_int(0)
+    f(_ip(job), _ip(iverb), _ip(maxit), _ip(nsrc), _ip(nx), _ip(ny), _ip(nz), _dp(tol), _dp(h),
+      _dp(x0), _dp(y0), _dp(z0), keep[0][1], keep[1][1], keep[2][1], keep[3][1], slow_p, u_p, C.byref(ierr))
+    return ierr.value
+
+
+def locate_l2_gridsearch(ldgrd, ngrd, nobs, iwantOT, t0use, mask, tobs, tcorr, varobs, test, t0, objfn):
+    """locate_l2_gridSearch__double64 (locate.c:923-1047) on the GPU; returns ierr.
+    t0/objfn/test must be 64-byte aligned float64 arrays, as the reference requires."""
+    L = _lib.lib()
+    m = np.ascontiguousarray(mask, dtype=np.int32)
+    to, tp = _arr(tobs)
+    va, vp = _arr(varobs)
+    tc, tcp = (None, None) if tcorr is None else _arr(tcorr)
+    return L.locate_l2_gridSearch__double64(int(ldgrd), int(ngrd), int(nobs), int(iwantOT), float(t0use),
+                                            m.ctypes.data_as(C.c_void_p), tp, tcp, vp,
+                                            test.ctypes.data_as(C.c_void_p), t0.ctypes.data_as(C.c_void_p),
+                                            objfn.ctypes.data_as(C.c_void_p))
+
+
+def aligned_empty(n, dtype=np.float64, align=64):
+    """numpy array whose data pointer is `align`-byte aligned (locate.c:967-974 requirement)."""
+    itemsize = np.dtype(dtype).itemsize
+    raw = np.zeros(n + align // itemsize, dtype=dtype)
+    off = (-raw.ctypes.data % align) // itemsize
+    return raw[off:off + n]
+
+
+class BatchSolver:
+    """Batched FSM solves on one GPU.  Tensors are torch CUDA(HIP) tensors.
+
+    sources: [nstat, nsrc, 4] float64 (ts, xs, ys, zs)
+    slow   : mode 'field': [nmodel, nz, ny, nx] (float32 or float64 = precision)
+             mode 'cells': [nmodel, ncz, ncy, ncx] float32 slowness per inversion cell
+    """
+
+    def __init__(self, nx, ny, nz, h, x0=0.0, y0=0.0, z0=0.0, maxit=50, tol=1e-8, precision=32,
+                 nref=None):
+        self.nx, self.ny, self.nz, self.h = int(nx), int(ny), int(nz), float(h)
+        self.x0, self.y0, self.z0 = float(x0), float(y0), float(z0)
+        self.maxit, self.tol, self.precision = int(maxit), float(tol), int(precision)
+        self.nref = nref
+        self._ws = None
+
+    def describe(self, nmodel, nstat, nsrc, slow_mode, nev=0, max_sweeps=-1):
+        b = _lib.FsmBatch()
+        b.nx, b.ny, b.nz = self.nx, self.ny, self.nz
+        b.h, b.x0, b.y0, b.z0 = self.h, self.x0, self.y0, self.z0
+        b.maxit, b.tol, b.precision = self.maxit, self.tol, self.precision
+        b.nmodel, b.nstat, b.nsrc = nmodel, nstat, nsrc
+        b.slow_mode = slow_mode
+        nr = self.nref or (1, 1, 1)
+        b.nrx, b.nry, b.nrz = nr
+        b.nev = nev
+        b.max_sweeps = max_sweeps
+        return b
+
+    def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None):
+        import torch
+        dev = slow.device
+        sources = sources.to(device=dev, dtype=torch.float64).contiguous()
+        nstat, nsrc = int(sources.shape[0]), int(sources.shape[1])
+        nmodel = int(slow.shape[0])
+        slow_mode = 1 if self.nref is not None else 0
+        want_dtype = torch.float64 if self.precision == 64 else torch.float32
+        if slow_mode == 0 and slow.dtype != want_dtype:
+            raise TypeError(f"slowness field must be {want_dtype} for precision {self.precision}")
+        if slow_mode == 1 and slow.dtype != torch.float32:
+            raise TypeError("cell slowness must be float32")
+        slow = slow.contiguous()
+        nev = 0 if ev_node is None else int(ev_node.numel())
+        b = self.describe(nmodel, nstat, nsrc, slow_mode, nev, max_sweeps)
+        nsolve = nmodel * nstat
+        niter = torch.zeros(nsolve, dtype=torch.int32, device=dev)
+        ierr = torch.zeros(nsolve, dtype=torch.int32, device=dev)
+        out = {"niter": niter, "ierr": ierr}
+        b.src = sources.data_ptr()
+        b.slow = slow.data_ptr()
+        b.niter, b.ierr = niter.data_ptr(), ierr.data_ptr()
+        if nev:
+            ev_node = ev_node.to(device=dev, dtype=torch.int32).contiguous()
+            ttab = torch.empty((nsolve, nev), dtype=torch.float32, device=dev)
+            b.ev_node, b.ttab = ev_node.data_ptr(), ttab.data_ptr()
+            out["ttab"] = ttab
+            out["_ev"] = ev_node
+        if want_fields:
+            u = torch.empty((nsolve, self.nz, self.ny, self.nx), dtype=want_dtype, device=dev)
+            b.u_out = u.data_ptr()
+            out["u"] = u
+        L = _lib.lib()
+        nbytes = L.mceik_fsm_workspace_bytes(C.byref(b))
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        rc = L.mceik_fsm_batch_solve(C.byref(b), self._ws.data_ptr(), nbytes, C.c_void_p(st))
+        if rc != 0:
+            raise RuntimeError(f"mceik_fsm_batch_solve failed ({rc})")
+        out["_keep"] = (sources, slow)
+        out["bytes_per_node_sweep"] = L.mceik_fsm_bytes_per_node_sweep(C.byref(b))
+        return out

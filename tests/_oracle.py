@@ -30,6 +30,10 @@ def lib():
             f = getattr(L, name)
             f.restype = C.c_int
             f.argtypes = [C.c_int] * 5 + [C.c_double] * 5 + [C.c_void_p] * 7
+        for name in ("oracle_eikonal3d_solve_dbg_f64", "oracle_eikonal3d_solve_dbg_f32"):
+            f = getattr(L, name)
+            f.restype = C.c_int
+            f.argtypes = [C.c_int] * 6 + [C.c_double] * 5 + [C.c_void_p] * 7
         L.oracle_batch_solve_f64.restype = C.c_int
         L.oracle_batch_solve_f64.argtypes = ([C.c_int] * 5 + [C.c_double] * 5 + [C.c_void_p] * 6
                                              + [C.c_int, C.c_int])
@@ -50,15 +54,16 @@ def lib():
 
 
 def eikonal_solve(nx, ny, nz, slow, h, sources, maxit=50, tol=1e-8, x0=0.0, y0=0.0, z0=0.0,
-                  dtype=np.float64):
-    """Serial-driver job 2 semantics (SETBCS + FSM). Returns (u, ierr, niter)."""
+                  dtype=np.float64, max_sweeps=-1):
+    """Serial-driver job 2 semantics (SETBCS + FSM). Returns (u, ierr, niter).
+    max_sweeps >= 0 stops after that many sweeps (debug bisection)."""
     src = np.atleast_2d(np.asarray(sources, dtype=np.float64))
     cols = [np.ascontiguousarray(src[:, k]) for k in range(4)]
     slow = np.ascontiguousarray(slow, dtype=dtype)
     u = np.zeros(nx * ny * nz, dtype=dtype)
     it = C.c_int(0)
-    f = lib().oracle_eikonal3d_solve_f64 if dtype == np.float64 else lib().oracle_eikonal3d_solve_f32
-    ierr = f(maxit, len(cols[0]), nx, ny, nz, tol, h, x0, y0, z0, *[_p(c) for c in cols],
+    f = lib().oracle_eikonal3d_solve_dbg_f64 if dtype == np.float64 else lib().oracle_eikonal3d_solve_dbg_f32
+    ierr = f(maxit, max_sweeps, len(cols[0]), nx, ny, nz, tol, h, x0, y0, z0, *[_p(c) for c in cols],
              _p(slow), _p(u), C.byref(it))
     return u, ierr, it.value
 

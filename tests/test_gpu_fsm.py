@@ -1,0 +1,221 @@
+"""GPU parity of the batched FSM kernel (libmceik_hip.so) against the oracle.
+
+* fp32 path: BITWISE equal to the fp32 twin (oracle/fsm_impl.inc, STABLE_UPDATE),
+  fields, iteration counts and ierr; within the stated tolerance of fp64.
+* fp64 path: BITWISE equal to the reference's own outputs (tests/golden) and
+  to the fp64 oracle.
+On a mismatch the test bisects the sweep budget to name the first bad sweep.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _solver(nx, ny, nz, h, precision, maxit=50, tol=1e-8, nref=None):
+    from mceik_amd.eikonal import BatchSolver
+    return BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, maxit, tol, precision, nref=nref)
+
+
+def _hetero(nx, ny, nz):
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    return 3000.0 + 4000.0 * k / (nz - 1) + 500.0 * np.sin(0.3 * i) * np.cos(0.25 * j) * np.sin(0.2 * k)
+
+
+def _rough(nx, ny, nz, seed):
+    return 2000.0 + 4000.0 * np.random.default_rng(seed).random((nz, ny, nx))
+
+
+def _first_bad_sweep(nx, ny, nz, h, slow32, src, maxit, tol):
+    """Smallest sweep budget at which GPU and twin differ (debug aid)."""
+    dev = _dev()
+    bs = _solver(nx, ny, nz, h, 32, maxit, tol)
+    for ms in range(0, 8 * maxit + 1):
+        out = bs.solve(torch.tensor(src[None]), torch.tensor(slow32.reshape(1, nz, ny, nx), device=dev),
+                       want_fields=True, max_sweeps=ms)
+        g = out["u"].cpu().numpy().ravel()
+        t, _, _ = O.eikonal_solve(nx, ny, nz, slow32, h, src, maxit=maxit, tol=tol, dtype=np.float32,
+                                  max_sweeps=ms)
+        if not np.array_equal(g.view(np.uint32), t.view(np.uint32)):
+            bad = np.flatnonzero(g.view(np.uint32) != t.view(np.uint32))
+            i = bad[0]
+            return ms, len(bad), (i % nx, (i // nx) % ny, i // (nx * ny)), g[i], t[i]
+    return None
+
+
+CASES = [
+    # (name, nx, ny, nz, velocity, sources[(ts,xs,ys,zs)...], maxit, tol)
+    ("hetero_16^3_top", 16, 16, 16, "hetero", [(0.0, 737.0, 689.0, 1500.0)], 50, 1e-8),
+    ("hetero_17x19x23", 17, 19, 23, "hetero", [(0.0, 837.0, 889.0, 2200.0)], 50, 1e-8),
+    ("rough_24x20x16_onnode", 24, 20, 16, "rough", [(0.0, 1100.0, 600.0, 900.0)], 50, 1e-8),
+    ("rough_13x9x11_xmax", 13, 9, 11, "rough", [(0.25, 1200.0, 330.0, 470.0)], 50, 1e-8),
+    ("hetero_21x18x15_2src", 21, 18, 15, "hetero", [(0.0, 420.0, 390.0, 200.0), (0.05, 1550.0, 1225.0, 1160.0)], 50, 1e-8),
+    ("rough_9x10x8_loose", 9, 10, 8, "rough", [(0.0, 260.0, 710.0, 40.0)], 50, 1e-3),
+    ("hetero_40x33x90_deep", 40, 33, 90, "hetero", [(0.0, 2050.0, 1630.0, 8900.0)], 50, 1e-8),
+    ("rough_70x12x30_wide", 70, 12, 30, "rough", [(0.0, 10.0, 1100.0, 2900.0)], 50, 1e-8),
+    ("hetero_33x41x25_maxit2", 33, 41, 25, "hetero", [(0.0, 1610.0, 2030.0, 1240.0)], 2, 1e-8),
+]
+
+
+def _case_slow(kind, nx, ny, nz, seed=1):
+    v = _hetero(nx, ny, nz) if kind == "hetero" else _rough(nx, ny, nz, seed)
+    return (1.0 / v).ravel()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fp32_bitwise_vs_twin(case):
+    name, nx, ny, nz, kind, srcs, maxit, tol = case
+    dev = _dev()
+    h = 100.0
+    slow32 = _case_slow(kind, nx, ny, nz).astype(np.float32)
+    src = np.asarray(srcs, dtype=np.float64)
+    bs = _solver(nx, ny, nz, h, 32, maxit, tol)
+    out = bs.solve(torch.tensor(src[None]), torch.tensor(slow32.reshape(1, nz, ny, nx), device=dev),
+                   want_fields=True)
+    g = out["u"].cpu().numpy().ravel()
+    t, ierr, it = O.eikonal_solve(nx, ny, nz, slow32, h, src, maxit=maxit, tol=tol, dtype=np.float32)
+    if not np.array_equal(g.view(np.uint32), t.view(np.uint32)):
+        pytest.fail(f"{name}: fields differ; first bad sweep: {_first_bad_sweep(nx, ny, nz, h, slow32, src, maxit, tol)}")
+    assert int(out["niter"][0]) == it
+    assert int(out["ierr"][0]) == ierr
+
+
+def test_fp32_batch_many_models_and_stations():
+    """nmodel x nstat solves in one launch (more solves than resident waves is
+    not needed here; the work queue path is the same)."""
+    dev = _dev()
+    nx, ny, nz, h = 20, 18, 22, 100.0
+    rng = np.random.default_rng(3)
+    nmodel, nstat = 3, 5
+    slows = np.stack([(1.0 / _rough(nx, ny, nz, 10 + m)).ravel().astype(np.float32) for m in range(nmodel)])
+    src = np.stack([np.array([[0.0, rng.uniform(0, 1900), rng.uniform(0, 1700), rng.uniform(0, 2100)]])
+                    for _ in range(nstat)])
+    ev = rng.integers(0, nx * ny * nz, 7).astype(np.int32)
+    bs = _solver(nx, ny, nz, h, 32)
+    out = bs.solve(torch.tensor(src), torch.tensor(slows.reshape(nmodel, nz, ny, nx), device=dev),
+                   ev_node=torch.tensor(ev), want_fields=True)
+    u = out["u"].cpu().numpy().reshape(nmodel * nstat, -1)
+    tt = out["ttab"].cpu().numpy()
+    for m in range(nmodel):
+        for s in range(nstat):
+            t, ierr, it = O.eikonal_solve(nx, ny, nz, slows[m], h, src[s], dtype=np.float32)
+            k = m * nstat + s
+            assert np.array_equal(u[k].view(np.uint32), t.view(np.uint32)), (m, s)
+            assert np.array_equal(tt[k].view(np.uint32), t[ev].view(np.uint32))
+            assert int(out["niter"][k]) == it
+
+
+def test_fp32_inversion_grid_mode_bitwise():
+    """slow_mode 1: per-cell slowness (nref refinement) == twin on the expanded field."""
+    dev = _dev()
+    nx, ny, nz, h, nref = 30, 26, 34, 100.0, (4, 4, 4)
+    ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
+    rng = np.random.default_rng(9)
+    v = rng.integers(2500, 6500, (ncz, ncy, ncx)).astype(np.int32)
+    scell = (1.0 / v.astype(np.float32)).astype(np.float32)
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    sfield = scell[k // nref[2], j // nref[1], i // nref[0]].ravel()
+    src = np.array([[[0.0, 1234.5, 987.6, (nz - 1) * h]], [[0.0, 300.0, 2200.0, (nz - 1) * h]]])
+    bs = _solver(nx, ny, nz, h, 32, nref=nref)
+    out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(1, -1), device=dev), want_fields=True)
+    u = out["u"].cpu().numpy().reshape(2, -1)
+    for s in range(2):
+        t, _, it = O.eikonal_solve(nx, ny, nz, sfield, h, src[s], dtype=np.float32)
+        assert np.array_equal(u[s].view(np.uint32), t.view(np.uint32)), s
+        assert int(out["niter"][s]) == it
+
+
+FSM_FILES = sorted(glob.glob(os.path.join(GOLD, "fsm_*.npz")))
+
+
+@pytest.mark.parametrize("path", FSM_FILES, ids=[os.path.basename(p)[4:-4] for p in FSM_FILES])
+def test_fp64_serial_driver_bitwise_vs_reference(path):
+    """The drop-in eikonal3d_serial_driver reproduces the reference's own output bit for bit."""
+    from mceik_amd.eikonal import eikonal3d_serial_driver
+    _dev()
+    g = dict(np.load(path, allow_pickle=False))
+    nx, ny, nz = int(g["nx"]), int(g["ny"]), int(g["nz"])
+    if "slow" in g:
+        slow = g["slow"]
+    elif str(g["velocity_formula"]) == "uniform":
+        slow = np.full(nx * ny * nz, 1.0 / float(g["velocity_const"]))
+    else:
+        slow = (1.0 / _hetero(nx, ny, nz)).ravel()
+    s = g["sources"]
+    u = np.zeros(nx * ny * nz)
+    args = (int(g["maxit"]), len(s), nx, ny, nz, float(g["tol"]), float(g["h"]), 0.0, 0.0, 0.0,
+            s[:, 0], s[:, 1], s[:, 2], s[:, 3], slow, u)
+    assert eikonal3d_serial_driver(1, 0, *args) == 0
+    assert eikonal3d_serial_driver(1, 0, *args) == 1          # already initialised
+    ierr = eikonal3d_serial_driver(2, 0, *args)
+    eikonal3d_serial_driver(3, 0, *args)
+    assert eikonal3d_serial_driver(2, 0, *args) == 1          # not initialised
+    assert ierr == int(g["ierr"])
+    if "u" in g:
+        assert np.array_equal(u.view(np.uint64), g["u"].view(np.uint64))
+    else:
+        assert np.array_equal(u[g["sample_idx"]].view(np.uint64), g["sample_u"].view(np.uint64))
+        if "xfsm3d" in path:
+            assert u.max() == 1.4308203212738235
+
+
+def test_fp32_serial_driver_within_tolerance():
+    from mceik_amd.eikonal import eikonal3d_serial_driver
+    _dev()
+    g = dict(np.load(os.path.join(GOLD, "fsm_hetero_17x19x23.npz"), allow_pickle=False))
+    nx, ny, nz = int(g["nx"]), int(g["ny"]), int(g["nz"])
+    s = g["sources"]
+    u = np.zeros(nx * ny * nz)
+    args = (50, 1, nx, ny, nz, 1e-8, 100.0, 0.0, 0.0, 0.0, s[:, 0], s[:, 1], s[:, 2], s[:, 3], g["slow"], u)
+    eikonal3d_serial_driver(1, 0, *args, precision=32)
+    assert eikonal3d_serial_driver(2, 0, *args, precision=32) == 0
+    eikonal3d_serial_driver(3, 0, *args, precision=32)
+    ref = g["u"]
+    assert np.all(np.abs(u - ref) <= 1e-6 * ref + 1e-7)
+
+
+def test_fp32_128cube_vs_twin_and_fp64():
+    """Headline grid size: two stations of one heterogeneous 128^3 model."""
+    dev = _dev()
+    n, h = 128, 100.0
+    slow64 = (1.0 / _hetero(n, n, n)).ravel()
+    slow32 = slow64.astype(np.float32)
+    src = np.array([[[0.0, h * 64 + 37.0, h * 64 - 11.0, h * 127]], [[0.0, 2345.0, 9876.0, h * 127]]])
+    bs = _solver(n, n, n, h, 32)
+    out = bs.solve(torch.tensor(src), torch.tensor(slow32.reshape(1, n, n, n), device=dev), want_fields=True)
+    u = out["u"].cpu().numpy().reshape(2, -1)
+    t, _, it = O.eikonal_solve(n, n, n, slow32, h, src[0], dtype=np.float32)
+    assert np.array_equal(u[0].view(np.uint32), t.view(np.uint32))
+    assert int(out["niter"][0]) == it
+    r, _, _ = O.eikonal_solve(n, n, n, slow64, h, src[0])
+    assert np.all(np.abs(u[0] - r) <= 1e-6 * r + 1e-7)
+
+
+def test_locate_l2_gpu_bitwise_vs_reference():
+    from mceik_amd.eikonal import aligned_empty, locate_l2_gridsearch
+    _dev()
+    g = dict(np.load(os.path.join(GOLD, "locate_l2.npz"), allow_pickle=False))
+    ld, ng, no = int(g["ldgrd"]), int(g["ngrd"]), int(g["nobs"])
+    test = aligned_empty(g["test"].size); test[:] = g["test"]
+    t0 = aligned_empty(ng); obj = aligned_empty(ng)
+    assert locate_l2_gridsearch(ld, ng, no, 1, 0.0, g["mask"], g["tobs"], g["tcorr"], g["varobs"], test, t0, obj) == 0
+    assert np.array_equal(t0.view(np.uint64), g["ot_t0"].view(np.uint64))
+    assert np.array_equal(obj.view(np.uint64), g["ot_objfn"].view(np.uint64))
+    assert locate_l2_gridsearch(ld, ng, no, 0, 4.0, np.zeros(no), g["tobs"], None, g["varobs"], test, t0, obj) == 0
+    assert np.array_equal(obj.view(np.uint64), g["fixed_objfn"].view(np.uint64))
+    # reference error behaviour: ldgrd*8 % 64 != 0
+    assert locate_l2_gridsearch(ld + 1, ng, no, 1, 0.0, g["mask"], g["tobs"], None, g["varobs"], test, t0, obj) == 1
