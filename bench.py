@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MCMC proposals/s (FSM eikonal + likelihood), BASELINE.json.
+
+One step = one proposal for every chain on every GPU: propose (one inversion
+cell per chain) -> batched FSM solves (chains x stations, HIP, fp32) ->
+travel times at the events -> L2 misfit with analytic origin time ->
+Metropolis.  N=1 runs configs[2] ("C3": 1024 chains, 128^3, 32 stations);
+--gpus N keeps 1024 chains per GPU (weak scaling; N=8 is configs[3], 8192
+chains) and gathers the kept posterior states to rank 0 over RCCL at the
+end of the timed region (the checkpoint).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+
+
+# ---------------------------------------------------------------- CPU baseline
+def _ref_solve_worker(args):
+    """One fp64 solve by the REFERENCE's own eikonal3d_serial_driver
+    (oracle/_ref/libfsm3d_ref.so, built from fsm3d.f90); single-threaded."""
+    so, n, h, src, slow_path = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    lib = C.CDLL(so)
+    slow = np.load(slow_path)
+    u = np.zeros(n ** 3)
+    i = lambda v: C.byref(C.c_int(v))
+    d = lambda v: C.byref(C.c_double(v))
+    ts, xs, ys, zs = (np.array([v]) for v in src)
+    P = lambda a: a.ctypes.data_as(C.c_void_p)
+    ierr = C.c_int(0)
+    args_ = lambda job: (i(job), i(0), i(50), i(1), i(n), i(n), i(n), d(1e-8), d(h), d(0.0), d(0.0), d(0.0),
+                         P(ts), P(xs), P(ys), P(zs), P(slow), P(u), C.byref(ierr))
+    lib.eikonal3d_serial_driver(*args_(1))
+    t = time.perf_counter()
+    lib.eikonal3d_serial_driver(*args_(2))
+    dt = time.perf_counter() - t
+    lib.eikonal3d_serial_driver(*args_(3))
+    return dt, ierr.value
+
+
+def cpu_baseline(p, v0, cores):
+    """Reference proposals/s on this host: `cores` single-threaded fp64 solves in
+    parallel (the reference's table-parallel design, mpiutils.f90:147-149),
+    proposals/s = solves/s / stations.  Runs before the GPU is initialised."""
+    import multiprocessing as mp
+    import tempfile
+    k, j, i = np.meshgrid(np.arange(p.nz), np.arange(p.ny), np.arange(p.nx), indexing="ij")
+    cell = ((k // p.nrz) * p.ncy + j // p.nry) * p.ncx + i // p.nrx
+    slow = np.ascontiguousarray((1.0 / v0[cell.ravel()].astype(np.float64)))
+    srcs = [(0.0, p.sx[s % p.nstat], p.sy[s % p.nstat], p.sz[s % p.nstat]) for s in range(cores)]
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libfsm3d_ref.so")
+    sample = f"{cores} fp64 solves (128^3 model of chain 0, stations 0..{cores - 1}), 1 thread each"
+    if os.path.exists(ref_so):
+        with tempfile.TemporaryDirectory() as td:
+            sp = os.path.join(td, "slow.npy")
+            np.save(sp, slow)
+            ctx = mp.get_context("spawn")
+            with ctx.Pool(cores) as pool:
+                t = time.perf_counter()
+                res = pool.map(_ref_solve_worker, [(ref_so, p.nx, p.h, s, sp) for s in srcs])
+                wall = time.perf_counter() - t
+        kind = "reference"
+        cpu_s = sum(r[0] for r in res)
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        L = O.lib()
+        xs = np.array([s[1] for s in srcs]); ys = np.array([s[2] for s in srcs]); zs = np.array([s[3] for s in srcs])
+        out = np.zeros(cores)
+        idx = np.zeros(cores, np.int32)
+        t = time.perf_counter()
+        L.oracle_batch_solve_f64(cores, 50, p.nx, p.ny, p.nz, 1e-8, p.h, 0.0, 0.0, 0.0, O._p(xs), O._p(ys),
+                                 O._p(zs), O._p(slow), O._p(idx), O._p(out), 0, cores)
+        wall = time.perf_counter() - t
+        kind = "port"
+        cpu_s = wall * cores
+    return {"value": round(cores / wall / p.nstat, 5), "unit": "proposals/s", "cores": cores, "kind": kind,
+            "sample": f"{sample}; wall {wall:.2f} s, {cpu_s:.1f} CPU-s; proposals/s = solves/s / {p.nstat} stations"}
+
+
+# ---------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--chains", type=int, default=0, help="chains per GPU (default: the config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cores", type=int, default=0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    from mceik_amd import mcmc
+
+    cfg = mcmc.CONFIGS[args.config]
+    per_gpu = args.chains or (cfg["nchains"] if args.config != "C4" else cfg["nchains"] // 8)
+    # problem geometry and start models are pure numpy: the CPU baseline runs
+    # before anything touches the GPU (its workers are spawned processes)
+    p = mcmc.make_problem(args.config, picks="analytic")
+    lo, hi = mcmc.shard(per_gpu * world, rank, world)
+    v0 = mcmc.initial_models(p, range(lo, hi))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = args.cpu_cores or int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(p, v0[0], cores)
+
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    # picks from the GPU forward of the true model (replaces the analytic ones)
+    tt = mcmc.picks_from_forward(local_rank)(p)
+    rng = np.random.default_rng(p.seed + 1)
+    p.tobs = tt.T.ravel().astype(np.float64) + rng.normal(0.0, 0.05, p.nevents * p.nstat)
+    p.nburn, p.keepk = args.warmup, max(1, args.steps)
+    smp = mcmc.Sampler(p, nchains=hi - lo, chain_offset=lo, v0=v0, max_samples=1, device=local_rank)
+    stream = torch.cuda.current_stream(dev)
+    smp.set_stream(stream.cuda_stream)
+    post = torch.empty((hi - lo, p.ncell), dtype=torch.int32, device=dev)
+    gathered = ([torch.empty_like(post) for _ in range(world)] if rank == 0 else None) if world > 1 else None
+
+    if args.warmup:
+        smp.run(args.warmup)
+    smp.fsm_stats(reset=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    smp.run(args.steps)
+    # checkpoint: the kept posterior states of every chain -> rank 0 (RCCL over xGMI)
+    smp.samples(max_states=1, device_ptr=post.data_ptr())
+    if world > 1:
+        dist.gather(post, gathered, dst=0)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    fsm_ms, nlaunch, iters = smp.fsm_stats()
+    _, logl, nacc, _ = smp.state()
+    smp.close()
+
+    if rank == 0:
+        n_nodes = p.nx * p.ny * p.nz
+        total = per_gpu * world * args.steps
+        from mceik_amd import _lib
+        b = _lib.FsmBatch(); b.precision = 32; b.slow_mode = 1; b.nstat = p.nstat
+        b.nrx, b.nry, b.nrz = p.nref
+        bpn = _lib.lib().mceik_fsm_bytes_per_node_sweep(C.byref(b))
+        alg_bytes = iters * 8.0 * n_nodes * bpn          # this rank's launches
+        avg_ms = fsm_ms / max(nlaunch, 1)
+        achieved = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                tj = json.load(f)
+            if tj.get("workload") == args.config and tj.get("chains_per_gpu") == per_gpu:
+                traffic = tj.get("hbm_bytes_per_launch")
+        line = {
+            "metric": METRIC,
+            "value": round(total / elapsed, 3),
+            "unit": "proposals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY s.8d heterogeneous model, picks = GPU forward of the true model + N(0,0.05 s))",
+            "config": {"workload": f"{args.config}: {per_gpu} chains/GPU, {p.nx}^3 grid, {p.nstat} stations, "
+                                   f"{p.nevents} events, nref=4",
+                       "chains_per_gpu": per_gpu, "chains_total": per_gpu * world, "grid": [p.nx, p.ny, p.nz],
+                       "stations": p.nstat, "events": p.nevents, "parallelism": f"chains sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "fsm_solve_kernel<float,1>",
+                         "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
+                         "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),
+                         "iterations_per_solve": round(iters / max(nlaunch, 1) / (per_gpu * p.nstat), 3)},
+            "cpu_baseline": cpu,
+            "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -50,6 +50,11 @@ int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max
 /* Diagnostics of the last step: device pointers (travel-time table, per-solve
  * iteration counts, accept flags) and sizes. */
 int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept);
+/* FSM accounting since init (or the last reset): kernel time of every FSM
+ * launch from hipEvents on the sampler's stream (ms), launches, and the
+ * sum over solves of executed iterations (8 sweeps each). Synchronises. */
+int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsigned long long *iters,
+                         int reset);
 int mceik_mcmc_finalize(mceik_mcmc **s);
 
 #ifdef __cplusplus

@@ -60,6 +60,7 @@ typedef struct mceik_fsm_batch {
     void *u_out;                /* device [nmodel*nstat][nx*ny*nz] or NULL   */
     int *niter, *ierr;          /* device [nmodel*nstat] or NULL             */
     int max_sweeps;             /* < 0: unlimited (debug)                    */
+    unsigned long long *iter_total;  /* device counter += iterations of every solve, or NULL */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */

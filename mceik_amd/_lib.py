@@ -22,7 +22,7 @@ class FsmBatch(C.Structure):
                 ("nrx", C.c_int), ("nry", C.c_int), ("nrz", C.c_int),
                 ("nev", C.c_int), ("ev_node", C.c_void_p), ("ttab", C.c_void_p),
                 ("u_out", C.c_void_p), ("niter", C.c_void_p), ("ierr", C.c_void_p),
-                ("max_sweeps", C.c_int)]
+                ("max_sweeps", C.c_int), ("iter_total", C.c_void_p)]
 
 
 class McmcParms(C.Structure):
@@ -69,7 +69,8 @@ class McmcOpts(C.Structure):
 EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "locate_l2_gridSearch__double64",
            "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
-           "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_finalize")
+           "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
+           "mceik_mcmc_finalize")
 
 
 def lib():
@@ -111,6 +112,9 @@ def lib():
     L.mceik_mcmc_get_samples.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, pi]
     L.mceik_mcmc_last.restype = C.c_int
     L.mceik_mcmc_last.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 3
+    L.mceik_mcmc_fsm_stats.restype = C.c_int
+    L.mceik_mcmc_fsm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong),
+                                       C.POINTER(C.c_ulonglong), C.c_int]
     L.mceik_mcmc_finalize.restype = C.c_int
     L.mceik_mcmc_finalize.argtypes = [C.POINTER(C.c_void_p)]
     _lib = L

@@ -75,6 +75,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.ncx = mceik_div_up(L.nx, L.nrx); L.ncy = mceik_div_up(L.ny, L.nry); L.ncz = mceik_div_up(L.nz, L.nrz);
     L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab;
     L.niter = b->niter; L.ierr = b->ierr;
+    L.iter_total = b->iter_total;
 }
 
 static int g_device_cus = 0;
@@ -360,6 +361,10 @@ out:
 // MCMC sampler (include/mceik.h)
 struct mceik_mcmc {
     McmcDev D;
+    std::vector<hipEvent_t> ev;        // pairs around FSM launches (timing)
+    size_t ev_used;
+    long long nlaunch;
+    unsigned long long *d_iters;
     mceik_fsm_batch fb;
     int device, max_samples, nburn, keepk, nkept;
     long long step;
@@ -395,9 +400,24 @@ static int source_index(int n, double x0, double dx, double xs)   // fsm3d.f90:6
     return (int)((xs - x0) / dx + 0.5);
 }
 
-static int mcmc_forward(mceik_mcmc *s)
+static int mcmc_forward(mceik_mcmc *s, bool timed)
 {
+    if (timed) {
+        if (s->ev_used + 2 > s->ev.size()) {
+            for (int i = 0; i < 64; i++) {
+                hipEvent_t e;
+                HIPCHK(hipEventCreate(&e));
+                s->ev.push_back(e);
+            }
+        }
+        HIPCHK(hipEventRecord(s->ev[s->ev_used], s->stream));
+    }
     if (mceik_fsm_batch_solve(&s->fb, s->ws, s->ws_bytes, s->stream)) return -1;
+    if (timed) {
+        HIPCHK(hipEventRecord(s->ev[s->ev_used + 1], s->stream));
+        s->ev_used += 2;
+        s->nlaunch++;
+    }
     return 0;
 }
 
@@ -486,6 +506,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     rc |= dalloc(s, &d_tt, (size_t)nch * nstat * nev);
     rc |= dalloc(s, &d_niter, (size_t)nch * nstat);
     rc |= dalloc(s, &d_ierr, (size_t)nch * nstat);
+    rc |= dalloc(s, &s->d_iters, 1);
     if (s->max_samples) {
         rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncell);
         rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
@@ -502,6 +523,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.slow_mode = 1; b.slow = D.slow_prop; b.nrx = nrx; b.nry = nry; b.nrz = nrz;
     b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = d_ierr;
     b.max_sweeps = -1;
+    b.iter_total = s->d_iters;
     s->ws_bytes = mceik_fsm_workspace_bytes(&b);
     if (hipMalloc(&s->ws, s->ws_bytes) != hipSuccess) {
         fprintf(stderr, "mceik_mcmc_init: cannot allocate %zu B of FSM workspace\n", s->ws_bytes);
@@ -509,10 +531,11 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         return -1;
     }
     // initial log-likelihood of every chain
-    if (mcmc_forward(s) || mcmc_init_loglik(D, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
+    if (mcmc_forward(s, false) || mcmc_init_loglik(D, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
         mceik_mcmc_finalize(&s);
         return -1;
     }
+    hipMemset(s->d_iters, 0, sizeof(unsigned long long));
     *out = s;
     return 0;
 }
@@ -530,7 +553,7 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
     for (int i = 0; i < nsteps; i++) {
         uint64_t step = (uint64_t)s->step;
         HIPCHK(mcmc_propose(s->D, step, s->stream));
-        if (mcmc_forward(s)) return -1;
+        if (mcmc_forward(s, true)) return -1;
         int slot = -1;
         if (s->max_samples && s->step >= s->nburn && (s->step - s->nburn) % s->keepk == 0) {
             slot = s->nkept % s->max_samples;
@@ -585,12 +608,37 @@ extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **ni
     return 0;
 }
 
+extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsigned long long *iters,
+                                    int reset)
+{
+    if (!s) return 1;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    double ms = 0.0;
+    for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
+        float t = 0.f;
+        HIPCHK(hipEventElapsedTime(&t, s->ev[i], s->ev[i + 1]));
+        ms += t;
+    }
+    unsigned long long it = 0;
+    HIPCHK(hipMemcpy(&it, s->d_iters, sizeof(it), hipMemcpyDeviceToHost));
+    if (fsm_ms) *fsm_ms = ms;
+    if (nlaunch) *nlaunch = s->nlaunch;
+    if (iters) *iters = it;
+    if (reset) {
+        s->ev_used = 0;
+        s->nlaunch = 0;
+        HIPCHK(hipMemset(s->d_iters, 0, sizeof(unsigned long long)));
+    }
+    return 0;
+}
+
 extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
 {
     if (!ps || !*ps) return 0;
     mceik_mcmc *s = *ps;
     hipStreamSynchronize(s->stream);
     for (void *p : s->allocs) hipFree(p);
+    for (hipEvent_t e : s->ev) hipEventDestroy(e);
     if (s->ws) hipFree(s->ws);
     delete s;
     *ps = nullptr;

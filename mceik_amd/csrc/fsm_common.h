@@ -32,6 +32,7 @@ struct FsmLaunch {
     int *niter;                  // [nsolve] iterations executed, may be null
     int *ierr;                   // [nsolve] reference ierr semantics, may be null
     unsigned *counter;           // work queue head (zeroed before the launch)
+    unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }

@@ -450,6 +450,7 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
         for (int o = 32; o > 0; o >>= 1) ierr = max(ierr, __shfl_xor(ierr, o, 64));
         if (!ok) ierr = 1;
         if (lane == 0) {
+            if (L.iter_total) atomicAdd(L.iter_total, (unsigned long long)iters);
             if (L.niter) L.niter[solve] = iters;
             if (L.ierr) L.ierr[solve] = ierr;
         }

@@ -292,6 +292,13 @@ class Sampler:
                 raise RuntimeError("mceik_memcpy failed")
         return ttab, niter, a
 
+    def fsm_stats(self, reset=False):
+        """(FSM kernel ms from hipEvents, launches, executed iterations summed over solves)."""
+        ms, nl, it = C.c_double(0), C.c_longlong(0), C.c_ulonglong(0)
+        if self._L.mceik_mcmc_fsm_stats(self._h, C.byref(ms), C.byref(nl), C.byref(it), int(reset)) != 0:
+            raise RuntimeError("mceik_mcmc_fsm_stats failed")
+        return ms.value, nl.value, it.value
+
     def samples(self, max_states=None, device_ptr=None):
         """Kept states [k, nchains, ncell] (host numpy, or copied into device_ptr)."""
         max_states = self.max_samples if max_states is None else max_states

@@ -23,6 +23,7 @@ def _problem(n=24, nstat=4, nev=6, seed=7):
     from mceik_amd import mcmc
     p = mcmc.make_problem("C2", n=n, nstat=nstat, nev=nev, seed=seed, picks=mcmc.picks_from_forward(0))
     p.dvmax = 400                       # large steps: both accepts and rejects in a few steps
+    p.var[:] = 1e-4                     # sharp likelihood so that some proposals are rejected
     return p
 
 
