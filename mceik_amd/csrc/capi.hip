@@ -73,6 +73,9 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.slow_mode = b->slow_mode;
     L.nrx = b->nrx > 0 ? b->nrx : 1; L.nry = b->nry > 0 ? b->nry : 1; L.nrz = b->nrz > 0 ? b->nrz : 1;
     L.ncx = mceik_div_up(L.nx, L.nrx); L.ncy = mceik_div_up(L.ny, L.nry); L.ncz = mceik_div_up(L.nz, L.nrz);
+    L.magic_rx = ((1u << 20) + L.nrx - 1) / L.nrx;
+    L.magic_ry = ((1u << 20) + L.nry - 1) / L.nry;
+    L.magic_rz = ((1u << 20) + L.nrz - 1) / L.nrz;
     L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab;
     L.niter = b->niter; L.ierr = b->ierr;
     L.iter_total = b->iter_total;
@@ -96,7 +99,7 @@ static int device_cus()
 // Waves a launch keeps resident (one solve each): occupancy x CUs, at most nsolve.
 static int batch_waves(const FsmLaunch &L, int is_double)
 {
-    size_t lds = MCEIK_MAX_SRC * 6 * 4 + (size_t)L.nzb * 64 * (is_double ? 8 : 4);
+    size_t lds = fsm_lds_bytes(L, is_double ? 8 : 4);
     int per_cu = fsm_occupancy(is_double, L.slow_mode, lds);
     if (per_cu < 1) per_cu = 1;
     long w = (long)per_cu * device_cus();
@@ -145,13 +148,22 @@ extern "C" double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b)
 extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes,
                                      void *stream)
 {
-    if (!b || b->nx < 2 || b->ny < 2 || b->nz < 2 || b->nsrc < 1 || b->nsrc > MCEIK_MAX_SRC ||
+    if (!b || b->nx < 2 || b->ny < 2 || b->nz < 2 || b->nx > 4096 || b->ny > 4096 || b->nz > 4096 ||
+        b->nsrc < 1 || b->nsrc > MCEIK_MAX_SRC ||
         b->nmodel < 1 || b->nstat < 1 || !(b->precision == 32 || b->precision == 64)) {
         fprintf(stderr, "mceik_fsm_batch_solve: invalid batch description\n");
         return 1;
     }
     if (b->slow_mode == 1 && b->precision != 32 && b->precision != 64) return 1;
     WsLayout w = ws_layout(b);
+    {
+        FsmLaunch G;
+        fill_launch(G, b);
+        if (G.field_elems * (b->precision == 64 ? 8 : 4) >= (size_t)1 << 31) {
+            fprintf(stderr, "mceik_fsm_batch_solve: one travel-time field must stay below 2 GiB\n");
+            return 1;
+        }
+    }
     if (!workspace || workspace_bytes < w.total) {
         fprintf(stderr, "mceik_fsm_batch_solve: workspace too small (%zu < %zu)\n", workspace_bytes, w.total);
         return 1;

@@ -22,6 +22,7 @@ struct FsmLaunch {
     int slow_mode;               // 0: per-node field (brick layout, R); 1: inversion grid (float)
     const void *slow;            // mode 0: [nmodel][field_elems] R ; mode 1: [nmodel][ncell] float
     int ncx, ncy, ncz, nrx, nry, nrz;
+    unsigned magic_rx, magic_ry, magic_rz;   // ceil(2^20 / nr*): cell = (node * magic) >> 20
     size_t field_elems;          // ntiles * nzb * 512
     void *u;                     // travel-time fields (brick layout, R)
     void *u0;                    // convergence side field (same layout)
@@ -36,6 +37,13 @@ struct FsmLaunch {
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
+
+// LDS of one solve wave: BC boxes, x halo column [nzb*8][8], staged f [8][64],
+// staged halos [8][8] + [8][2][8], lane trash [64]
+static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
+{
+    return (size_t)MCEIK_MAX_SRC * 6 * 4 + ((size_t)L.nzb * 64 + 512 + 64 + 128 + 64) * es;
+}
 
 // Fills the tile geometry of a launch from nx, ny, nz.
 static inline void fsm_geometry(FsmLaunch *L)

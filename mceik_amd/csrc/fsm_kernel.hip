@@ -95,87 +95,119 @@ __device__ __forceinline__ double godunov(double a, double b, double c, double f
     return UN;
 }
 
-// ---- 8-value column segments (32 B fp32 / 64 B fp64, always aligned) ------
-__device__ __forceinline__ void load8(const float *p, float (&v)[8])
+// ---- buffer resources: 32-bit offsets, out-of-range reads return 0 and
+// out-of-range writes are dropped, so predicated memory ops need no branches.
+#define OOB 0x80000000u
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+__device__ __forceinline__ Rsrc make_rsrc(const void *p, uint32_t bytes)
 {
-    float4 a = reinterpret_cast<const float4 *>(p)[0], b = reinterpret_cast<const float4 *>(p)[1];
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-__device__ __forceinline__ void store8(float *p, const float (&v)[8])
-{
-    reinterpret_cast<float4 *>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
-    reinterpret_cast<float4 *>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
-}
-__device__ __forceinline__ void load8(const double *p, double (&v)[8])
-{
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        double2 a = reinterpret_cast<const double2 *>(p)[i];
-        v[2 * i] = a.x; v[2 * i + 1] = a.y;
-    }
-}
-__device__ __forceinline__ void store8(double *p, const double (&v)[8])
-{
-#pragma unroll
-    for (int i = 0; i < 4; i++) reinterpret_cast<double2 *>(p)[i] = make_double2(v[2 * i], v[2 * i + 1]);
+    // wave-uniform by construction (kernel args / readfirstlane'd solve id)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, bytes, 0x00020000);
 }
 
+// NOTE (ROCm 7.2 clang): extracting elements of the uint4 returned by
+// __builtin_amdgcn_raw_buffer_load_b128 miscompiles into one buffer_load_dword;
+// bit-casting the whole vector to float4 / double2 keeps the dwordx4.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void bload8(Rsrc r, uint32_t off, float (&v)[8])
+{
+    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    f4v b = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, const float (&v)[8])
+{
+    f4v a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), r, off + 16, 0, 0);
+}
+__device__ __forceinline__ void bload8(Rsrc r, uint32_t off, double (&v)[8])
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        d2v a = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * k, 0, 0));
+        v[2 * k] = a.x; v[2 * k + 1] = a.y;
+    }
+}
+__device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, const double (&v)[8])
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        d2v a = {v[2 * k], v[2 * k + 1]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off + 16 * k, 0, 0);
+    }
+}
+__device__ __forceinline__ float bload1f(Rsrc r, uint32_t off)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// ---- lane exchange: x neighbours by DPP (lane -+ 1 in a 16-lane row),
+// y neighbours by ds_bpermute (lane -+ 8).  Tile-edge lanes get halo values.
+__device__ __forceinline__ float dpp_from_prev(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_next(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double dpp_from_prev(double v)
+{
+    unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x111, 0xf, 0xf, false);
+    unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x111, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double dpp_from_next(double v)
+{
+    unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x101, 0xf, 0xf, false);
+    unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x101, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 template <typename R>
-__device__ __forceinline__ R shfl_up_(R v, int d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ R shfl_up8(R v) { return __shfl_up(v, 8, 64); }
 template <typename R>
-__device__ __forceinline__ R shfl_down_(R v, int d) { return __shfl_down(v, d, 64); }
+__device__ __forceinline__ R shfl_down8(R v) { return __shfl_down(v, 8, 64); }
+
+// Branchless fp32 Godunov update (values and ierr identical to godunov(float)
+// above and to the twin): the 2D and 3D candidates are evaluated side by side,
+// so the two correctly rounded square roots are not serialised.
+__device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, int &ierr)
+{
+    const float UN = FLT_MAX;
+    const float a1 = fminf(fminf(a, b), c);
+    const float a3 = fmaxf(fmaxf(a, b), c);
+    const float a2 = __builtin_amdgcn_fmed3f(a, b, c);
+    const float d2 = a2 - a1, d3 = a3 - a1;
+    const float y2 = 0.5f * (d2 + __builtin_sqrtf((2.0f * f) * f - d2 * d2));
+    const float sm = d2 + d3;
+    const float q = ((d2 * d2) + (d3 * d3)) - f * f;
+    const float disc = sm * sm - 3.0f * q;
+    const float y3 = (sm + __builtin_sqrtf(disc)) * (1.0f / 3.0f);
+    const bool one = !(f > d2), two = !(y2 > d3);
+    const float y = one ? f : (two ? y2 : y3);
+    const float x = a1 + y;
+    const bool ok = x < UN;
+    const bool nan_in = a1 == UN;
+    ierr = nan_in ? 0 : (!ok ? 3 : ((!one && !two && disc < 0.0f) ? 1 : 0));
+    return (nan_in || !ok) ? UN : x;
+}
+__device__ __forceinline__ double godunov_bl(double a, double b, double c, double f, int &ierr)
+{
+    return godunov(a, b, c, f, ierr);   // fp64: the reference's literal form
+}
 
 // x-fastest node -> brick-layout element index
 __device__ __forceinline__ size_t brick_index(const FsmLaunch &L, int x, int y, int z)
 {
     int tile = (y >> 3) * L.ntx + (x >> 3);
     return ((((size_t)tile * L.nzb + (z >> 3)) * 64 + ((y & 7) * 8 + (x & 7))) << 3) + (z & 7);
-}
-
-// Where a lane stands in the tile/brick stream of one sweep.
-struct Brick {
-    bool valid;       // a real brick (not before/after the stream or z padding)
-    bool in_xy;       // this lane's column is inside the grid
-    bool xp, xn, yp, yn;   // sweep-upwind / sweep-downwind neighbour exists (grid edge rule)
-    int x, y, zb;     // physical column and z-brick
-    size_t seg;       // element offset of this lane's 8-value column segment
-    size_t hx_seg;    // x-downwind halo segment (lane lx=7), next tile
-    size_t hy_seg;    // y halo segment (ly=0: upwind tile, ly=7: downwind tile)
-};
-
-template <bool RZ>
-__device__ __forceinline__ Brick brick_at(const FsmLaunch &L, int vb, int lxs, int lys, int rx, int ry)
-{
-    Brick b;
-    b.valid = false; b.in_xy = false; b.xp = b.xn = b.yp = b.yn = false;
-    b.x = b.y = b.zb = 0; b.seg = b.hx_seg = b.hy_seg = 0;
-    if (vb < 0) return b;
-    int k = vb / L.sb, zbs = vb - k * L.sb;
-    if (k >= L.ntiles || zbs >= L.nzb) return b;
-    b.valid = true;
-    int tys = k / L.ntx, txs = k - tys * L.ntx;
-    int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
-    b.zb = RZ ? L.nzb - 1 - zbs : zbs;
-    int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
-    b.x = tx * 8 + lx; b.y = ty * 8 + ly;
-    b.in_xy = b.x < L.nx && b.y < L.ny;
-    bool xlo = b.x > 0, xhi = b.x < L.nx - 1, ylo = b.y > 0, yhi = b.y < L.ny - 1;
-    b.xp = rx ? xhi : xlo; b.xn = rx ? xlo : xhi;
-    b.yp = ry ? yhi : ylo; b.yn = ry ? ylo : yhi;
-    b.seg = ((((size_t)(ty * L.ntx + tx) * L.nzb + b.zb) * 64 + (ly * 8 + lx)) << 3);
-    // x-downwind halo: first column of the next tile in sweep order
-    int txn = rx ? tx - 1 : tx + 1, lxn = rx ? 7 : 0;
-    if (lxs == 7 && b.xn)
-        b.hx_seg = ((((size_t)(ty * L.ntx + txn) * L.nzb + b.zb) * 64 + (ly * 8 + lxn)) << 3);
-    // y halos: upwind tile's last row (new values), downwind tile's first row (old values)
-    if (lys == 0 && b.yp) {
-        int tyh = ry ? ty + 1 : ty - 1, lyh = ry ? 0 : 7;
-        b.hy_seg = ((((size_t)(tyh * L.ntx + tx) * L.nzb + b.zb) * 64 + (lyh * 8 + lx)) << 3);
-    } else if (lys == 7 && b.yn) {
-        int tyh = ry ? ty - 1 : ty + 1, lyh = ry ? 7 : 0;
-        b.hy_seg = ((((size_t)(tyh * L.ntx + tx) * L.nzb + b.zb) * 64 + (lyh * 8 + lx)) << 3);
-    }
-    return b;
 }
 
 // Per-solve boundary-condition boxes (EIKONAL3D_SETBCS nodes, lupd = .FALSE.).
@@ -186,33 +218,80 @@ struct BcBoxes {
 };
 #define BC_LDS_BYTES (MCEIK_MAX_SRC * 6 * 4)
 
-__device__ __forceinline__ bool in_bc_xy(const BcBoxes &bc, int k, int x, int y)
-{
-    const int *b = bc.box + 6 * k;
-    return x >= b[0] && x <= b[1] && y >= b[2] && y <= b[3];
-}
+// Position of a lane in the tile/brick stream of one sweep, advanced by one
+// virtual brick per macro step (no divisions in the loop).
+struct Pos {
+    int vb, k, zbs, txs, tys;
+};
 
-// Slowness*h for the 8 nodes of a lane's segment.
-template <typename R, int SLOWMODE>
-__device__ __forceinline__ void load_f(const FsmLaunch &L, const void *slow_model, const Brick &b,
-                                       R hr, R (&f)[8])
+__device__ __forceinline__ void pos_init(Pos &p, int vb, const FsmLaunch &L)
 {
-    if (SLOWMODE == 0) {
-        R s[8];
-        load8(reinterpret_cast<const R *>(slow_model) + b.seg, s);
-#pragma unroll
-        for (int i = 0; i < 8; i++) f[i] = s[i] * hr;
-    } else {
-        const float *si = reinterpret_cast<const float *>(slow_model);
-        int cx = min(b.x, L.nx - 1) / L.nrx, cy = min(b.y, L.ny - 1) / L.nry;
-        const float *col = si + (size_t)cy * L.ncx + cx;
-        size_t plane = (size_t)L.ncx * L.ncy;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            int z = min(b.zb * 8 + i, L.nz - 1);
-            f[i] = (R)col[(size_t)(z / L.nrz) * plane] * hr;
+    p.vb = vb;
+    int v = vb < 0 ? 0 : vb;
+    p.k = v / L.sb; p.zbs = v - p.k * L.sb;
+    p.tys = p.k / L.ntx; p.txs = p.k - p.tys * L.ntx;
+}
+__device__ __forceinline__ void pos_adv(Pos &p, const FsmLaunch &L)
+{
+    if (p.vb >= 0) {
+        if (++p.zbs == L.sb) {
+            p.zbs = 0; p.k++;
+            if (++p.txs == L.ntx) { p.txs = 0; p.tys++; }
         }
     }
+    p.vb++;
+}
+
+enum { F_VALID = 1, F_ACT = 2, F_XP = 4, F_XN = 8, F_YP = 16, F_YN = 32 };
+
+// What a lane needs about one of its bricks.
+struct BInfo {
+    uint32_t seg, hx, hy;    // byte offsets (u buffer): own segment, x-downwind halo, y halo (OOB if none)
+    int zb8, flags, x, y;    // bits 8..15 of flags: BC z-slots (physical) of this column segment
+};
+
+template <typename R, bool RZ>
+__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Pos &p, int lx, int ly, int lxs, int lys,
+                                            int rx, int ry, const BcBoxes &bc)
+{
+    BInfo b;
+    const bool valid = p.vb >= 0 && p.k < L.ntiles && p.zbs < L.nzb;
+    int tx = rx ? L.ntx - 1 - p.txs : p.txs, ty = ry ? L.nty - 1 - p.tys : p.tys;
+    int zb = RZ ? L.nzb - 1 - p.zbs : p.zbs;
+    if (!valid) { tx = 0; ty = 0; zb = 0; }
+    b.zb8 = zb * 8;
+    b.x = tx * 8 + lx; b.y = ty * 8 + ly;
+    const bool inxy = b.x < L.nx && b.y < L.ny;
+    const bool xlo = b.x > 0, xhi = b.x < L.nx - 1, ylo = b.y > 0, yhi = b.y < L.ny - 1;
+    const bool xp = rx ? xhi : xlo, xn = rx ? xlo : xhi, yp = ry ? yhi : ylo, yn = ry ? ylo : yhi;
+    int fl = (valid ? F_VALID : 0) | ((valid && inxy) ? F_ACT : 0) | (xp ? F_XP : 0) | (xn ? F_XN : 0) |
+             (yp ? F_YP : 0) | (yn ? F_YN : 0);
+    const uint32_t es = sizeof(R);
+    const uint32_t stride_tile = (uint32_t)L.nzb * 512u;
+    b.seg = valid ? ((uint32_t)(ty * L.ntx + tx) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lx) * 8u) * es : OOB;
+    b.hx = OOB;
+    if (valid && lxs == 7 && xn) {
+        int txn = rx ? tx - 1 : tx + 1, lxn = rx ? 7 : 0;
+        b.hx = ((uint32_t)(ty * L.ntx + txn) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lxn) * 8u) * es;
+    }
+    b.hy = OOB;
+    if (valid && ((lys == 0 && yp) || (lys == 7 && yn))) {
+        int tyh = (lys == 0) == (ry == 0) ? ty - 1 : ty + 1;
+        int lyh = (lys == 0) == (ry == 0) ? 7 : 0;
+        b.hy = ((uint32_t)(tyh * L.ntx + tx) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(lyh * 8 + lx) * 8u) * es;
+    }
+    // BC z-slots of this column segment
+    unsigned m = 0;
+    for (int k = 0; k < bc.n; k++) {
+        const int *q = bc.box + 6 * k;
+        if (b.x >= q[0] && b.x <= q[1] && b.y >= q[2] && b.y <= q[3]) {
+            int lo = q[4] - b.zb8, hi = q[5] - b.zb8;
+            lo = lo < 0 ? 0 : lo; hi = hi > 7 ? 7 : hi;
+            if (lo <= hi) m |= ((2u << hi) - (1u << lo));
+        }
+    }
+    b.flags = fl | (int)(m << 8);
+    return b;
 }
 
 template <typename R, int SLOWMODE>
@@ -224,130 +303,185 @@ __device__ __forceinline__ double slow_at(const FsmLaunch &L, const void *slow_m
     return (double)si[((size_t)(z / L.nrz) * L.ncy + y / L.nry) * L.ncx + x / L.nrx];
 }
 
+// Slowness of the 8 nodes of a segment (prefetch; multiplied by h when staged).
+template <typename R, int SLOWMODE>
+__device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, Rsrc sr, const BInfo &b, R (&s)[8])
+{
+    if (SLOWMODE == 0) {
+        bload8(sr, (b.flags & F_VALID) ? b.seg : OOB, s);
+    } else {
+        const uint32_t mx = L.magic_rx, my = L.magic_ry, mz = L.magic_rz;
+        const int x = b.x < L.nx ? b.x : L.nx - 1, y = b.y < L.ny ? b.y : L.ny - 1;
+        const uint32_t col = ((uint32_t)y * my >> 20) * (uint32_t)L.ncx + ((uint32_t)x * mx >> 20);
+        const uint32_t plane = (uint32_t)L.ncx * L.ncy;
+        const bool v = (b.flags & F_VALID) != 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            int z = b.zb8 + i;
+            z = z < L.nz ? z : L.nz - 1;
+            const uint32_t off = (col + ((uint32_t)z * mz >> 20) * plane) * 4u;
+            s[i] = (R)bload1f(sr, v ? off : OOB);
+        }
+    }
+}
+
 // One Gauss-Seidel sweep over the whole grid in direction (rx, ry, RZ).
 template <typename R, int SLOWMODE, bool RZ>
-__device__ __forceinline__ void sweep(const FsmLaunch &L, R *__restrict__ u, R *__restrict__ u0,
-                                      const void *slow_model, const BcBoxes &bc, R *xh,
+__device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
+                                      R *xh, R *sf, R *shx, R *shy, R *trash,
                                       int rx, int ry, bool first_sweep, bool last_sweep,
                                       bool &notconv, int &ierr_last)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
+    const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
     const R hr = (R)L.h, T = (R)L.conv_thresh, tolr = (R)L.tol;
     const int nmacro = L.ntiles * L.sb + 14;
+    const int hysel = lys >= 4;
 
-    R c[8], n[8], q[8], r[8], hx[8], hy[8], hxq[8], hyq[8], f[8], fq[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) { c[i] = n[i] = q[i] = r[i] = hx[i] = hy[i] = hxq[i] = hyq[i] = UN; f[i] = fq[i] = 0; }
-
-    // prologue: resident c = brick(vb0), n = brick(vb0+1), halo/f of vb0
+    R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8];
+    Pos p1;
+    pos_init(p1, -d, L);
+    BInfo b0 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
+    // prologue: c = brick(vb0), n = brick(vb0+1); stage f and halos of vb0
+    bload8(ur, b0.seg, c);
+    prefetch_slow<R, SLOWMODE>(L, sr, b0, fq);
+    bload8(ur, b0.hx, hxq);
+    bload8(ur, b0.hy, hyq);
+    pos_adv(p1, L);
     {
-        Brick b0 = brick_at<RZ>(L, -d, lxs, lys, rx, ry), b1 = brick_at<RZ>(L, 1 - d, lxs, lys, rx, ry);
-        if (b0.valid) {
-            load8(u + b0.seg, c);
-            load_f<R, SLOWMODE>(L, slow_model, b0, hr, f);
-            if (b0.hx_seg) load8(u + b0.hx_seg, hx);
-            if (b0.hy_seg) load8(u + b0.hy_seg, hy);
-        }
-        if (b1.valid) load8(u + b1.seg, n);
+        BInfo b1 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
+        bload8(ur, b1.seg, n);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) { r[i] = UN; sf[i * 64 + lane] = fq[i] * hr; }
+    if (lxs == 7) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) shx[i * 8 + lys] = hxq[i];
+    }
+    if (lys == 0 || lys == 7) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
     }
 
     for (int B = 0; B < nmacro; B++) {
-        const int vb = B - d;
-        const Brick b = brick_at<RZ>(L, vb, lxs, lys, rx, ry);
-        // prefetch: u of brick vb+2 (becomes n next step), halo + f of vb+1
+        // ---- prefetch: u of vb+2 (-> n next step); slowness and halos of vb+1
+        const BInfo b1 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
         {
-            Brick b1 = brick_at<RZ>(L, vb + 1, lxs, lys, rx, ry), b2 = brick_at<RZ>(L, vb + 2, lxs, lys, rx, ry);
-            if (b2.valid) load8(u + b2.seg, q);
-            if (b1.valid) {
-                load_f<R, SLOWMODE>(L, slow_model, b1, hr, fq);
-                if (b1.hx_seg) load8(u + b1.hx_seg, hxq);
-                if (b1.hy_seg) load8(u + b1.hy_seg, hyq);
+            Pos p2 = p1;
+            pos_adv(p2, L);
+            const bool v2 = p2.vb >= 0 && p2.k < L.ntiles && p2.zbs < L.nzb;
+            uint32_t seg2 = OOB;
+            if (v2) {
+                int tx = rx ? L.ntx - 1 - p2.txs : p2.txs, ty = ry ? L.nty - 1 - p2.tys : p2.tys;
+                int zb = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
+                seg2 = ((uint32_t)(ty * L.ntx + tx) * ((uint32_t)L.nzb * 512u) + (uint32_t)zb * 512u +
+                        (uint32_t)(ly * 8 + lx) * 8u) * (uint32_t)sizeof(R);
             }
+            bload8(ur, seg2, q);
         }
-        // BC membership of this column for each source box
-        unsigned bcxy = 0;
-        for (int k = 0; k < bc.n; k++) bcxy |= (in_bc_xy(bc, k, b.x, b.y) ? 1u : 0u) << k;
-        const bool colact = b.valid && b.in_xy;
+        prefetch_slow<R, SLOWMODE>(L, sr, b1, fq);
+        bload8(ur, b1.hx, hxq);
+        bload8(ur, b1.hy, hyq);
+
+        // ---- the 8 z-slots of the current brick
+        const int fl = b0.flags;
+        const bool act = (fl & F_ACT) != 0;
         bool changed = false;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            const int pj = RZ ? 7 - j : j;                 // physical slot of sweep slot j
-            const int pprev = RZ ? pj + 1 : pj - 1;         // physical slot of sweep slot j-1
-            const int pnext = RZ ? pj - 1 : pj + 1;         // physical slot of sweep slot j+1
-            const int zabs = b.zb * 8 + pj;
+            const int pj = RZ ? 7 - j : j;
+            const int pprev = RZ ? pj + 1 : pj - 1;
+            const int pnext = RZ ? pj - 1 : pj + 1;
+            const int zabs = b0.zb8 + pj;
             const R self = c[pj];
-            // neighbour lanes: upwind lanes are one brick ahead (their r[pj] still
-            // holds this brick's slot j), downwind lanes one brick behind (their n[pj])
-            const R xm = shfl_up_(r[pj], 1), xpv = shfl_down_(n[pj], 1);
-            const R ym = shfl_up_(r[pj], 8), ypv = shfl_down_(n[pj], 8);
-            R xup = self, xdn = self, yup = self, ydn = self, zup = self, zdn = self;
-            if (b.xp) xup = lxs > 0 ? xm : xh[zabs * 8 + lys];
-            if (b.xn) xdn = lxs < 7 ? xpv : hx[pj];
-            if (b.yp) yup = lys > 0 ? ym : hy[pj];
-            if (b.yn) ydn = lys < 7 ? ypv : hy[pj];
+            const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
+            const R ym = shfl_up8(r[pj]), ypv = shfl_down8(n[pj]);
+            const R fv = sf[pj * 64 + lane];
+            const R hxv = shx[pj * 8 + lys];
+            const R hyv = shy[(pj * 2 + hysel) * 8 + lxs];
+            const R xhv = xh[zabs * 8 + lys];
+            const R xup = !(fl & F_XP) ? self : (lxs > 0 ? xm : xhv);
+            const R xdn = !(fl & F_XN) ? self : (lxs < 7 ? xpv : hxv);
+            const R yup = !(fl & F_YP) ? self : (lys > 0 ? ym : hyv);
+            const R ydn = !(fl & F_YN) ? self : (lys < 7 ? ypv : hyv);
             const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
             const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
-            if (zp_ex) zup = j > 0 ? r[pprev] : r[RZ ? 0 : 7];
-            if (zn_ex) zdn = j < 7 ? c[pnext] : n[RZ ? 7 : 0];
+            const R zup = zp_ex ? (j > 0 ? r[pprev] : r[RZ ? 0 : 7]) : self;
+            const R zdn = zn_ex ? (j < 7 ? c[pnext] : n[RZ ? 7 : 0]) : self;
             const R ux = xup < xdn ? xup : xdn;
             const R uy = yup < ydn ? yup : ydn;
             const R uz = zup < zdn ? zup : zdn;
             int e;
-            const R ub = godunov(ux, uy, uz, f[pj], e);
-            bool isbc = false;
-            for (int k = 0; k < bc.n; k++)
-                isbc |= ((bcxy >> k) & 1u) && zabs >= bc.box[6 * k + 4] && zabs <= bc.box[6 * k + 5];
-            const bool upd = colact && zabs < L.nz && !isbc;
+            const R ub = godunov_bl(ux, uy, uz, fv, e);
+            const bool upd = act && zabs < L.nz && !((fl >> (8 + pj)) & 1);
             const R nv = upd ? (self < ub ? self : ub) : self;
             if (upd && nv < self && self >= T) notconv = true;
-            if (last_sweep && colact && b.x == 0 && b.y == 0 && zabs == 0) ierr_last = upd ? e : 0;
+            if (last_sweep && act && b0.x == 0 && b0.y == 0 && zabs == 0) ierr_last = upd ? e : 0;
             changed |= nv != self;
             r[pj] = nv;
-            if (lxs == 7 && b.valid) xh[zabs * 8 + lys] = nv;
+            // x-upwind halo of the next tile (lanes lx=7); other lanes write a private trash word
+            R *dst = (lxs == 7 && (fl & F_VALID)) ? xh + zabs * 8 + lys : trash + lane;
+            *dst = nv;
         }
-        if (b.valid) {
-            if (changed) store8(u + b.seg, r);
-            if (first_sweep) {
-                bool need = false;
+
+        // ---- write-back and convergence bookkeeping of the current brick
+        bstore8(ur, changed ? b0.seg : OOB, r);
+        if (first_sweep) {
+            bool need = false;
 #pragma unroll
-                for (int i = 0; i < 8; i++) need |= c[i] < T;
-                if (need) store8(u0 + b.seg, c);
+            for (int i = 0; i < 8; i++) need |= c[i] < T;
+            bstore8(u0r, need ? b0.seg : OOB, c);
+        }
+        if (last_sweep) {
+            bool need = false;
+            if (act && !notconv) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) need |= (r[i] < T) && (b0.zb8 + i < L.nz);
             }
-            if (last_sweep && !notconv && colact) {
-                bool need = false;
+            if (__any(need)) {
+                R v0[8];
+                bload8(u0r, need ? b0.seg : OOB, v0);
 #pragma unroll
-                for (int i = 0; i < 8; i++) need |= (r[i] < T) && (b.zb * 8 + i < L.nz);
-                if (need) {
-                    R v0[8];
-                    load8(u0 + b.seg, v0);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        R dlt = v0[i] - r[i];
-                        dlt = dlt < (R)0 ? -dlt : dlt;
-                        if (b.zb * 8 + i < L.nz && !(dlt < tolr)) notconv = true;
-                    }
+                for (int i = 0; i < 8; i++) {
+                    R dl = v0[i] - r[i];
+                    dl = dl < (R)0 ? -dl : dl;
+                    if (need && b0.zb8 + i < L.nz && !(dl < tolr)) notconv = true;
                 }
             }
         }
-        asm volatile("" ::: "memory");   // order LDS halo traffic across steps (one wave, in-order LDS)
+        asm volatile("" ::: "memory");
+        // ---- stage the prefetched slowness/halos of vb+1 for the next step
 #pragma unroll
-        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; hx[i] = hxq[i]; hy[i] = hyq[i]; f[i] = fq[i]; }
+        for (int i = 0; i < 8; i++) sf[i * 64 + lane] = fq[i] * hr;
+        if (lxs == 7) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) shx[i * 8 + lys] = hxq[i];
+        }
+        if (lys == 0 || lys == 7) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; }
+        b0 = b1;
+        pos_adv(p1, L);
     }
 }
 
 // ---- per-solve setup: u = u_nan, then the source boxes (EIKONAL3D_SETBCS) ----
 template <typename R, int SLOWMODE>
-__device__ bool init_field(const FsmLaunch &L, R *u, const void *slow_model, const double *src,
+__device__ bool init_field(const FsmLaunch &L, R *u, Rsrc ur, const void *slow_model, const double *src,
                            BcBoxes &bc)
 {
     const int lane = threadIdx.x;
     const R UN = Num<R>::unan();
-    const size_t nvec = L.field_elems / 8;
+    const uint32_t nvec = (uint32_t)(L.field_elems / 8);
     R fill[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) fill[i] = UN;
-    for (size_t i = lane; i < nvec; i += 64) store8(u + i * 8, fill);
+    for (uint32_t i = lane; i < nvec; i += 64) bstore8(ur, i * 8u * (uint32_t)sizeof(R), fill);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     bc.n = L.nsrc;
@@ -379,7 +513,7 @@ __device__ bool init_field(const FsmLaunch &L, R *u, const void *slow_model, con
             for (int i = 0; i < np; i++) { lo = min(lo, loc[a][i] - 1); hi = max(hi, loc[a][i] - 1); }
             if (lane == 0) { bc.box[6 * s + 2 * a] = lo; bc.box[6 * s + 2 * a + 1] = hi; }
         }
-        if (!ok) { bc.n = s; return false; }
+        if (!ok) { bc.n = s; break; }
         // lanes 0..26 each own one node of the 3x3x3 candidate box
         if (lane < 27) {
             int i = lane % 3, j = (lane / 3) % 3, k = lane / 9;
@@ -399,7 +533,8 @@ __device__ bool init_field(const FsmLaunch &L, R *u, const void *slow_model, con
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
-    return true;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    return ok;
 }
 
 template <typename R, int SLOWMODE>
@@ -407,23 +542,36 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int *bcbox = reinterpret_cast<int *>(smem);                 // 192 B, 16-B multiple
-    R *xh = reinterpret_cast<R *>(smem + BC_LDS_BYTES);
+    R *xh = reinterpret_cast<R *>(smem + BC_LDS_BYTES);         // [nzb*8][8]
+    R *sf = xh + (size_t)L.nzb * 64;                            // [8][64] staged f = s*h
+    R *shx = sf + 512;                                          // [8][8]   x-downwind halo
+    R *shy = shx + 64;                                          // [8][2][8] y halos
+    R *trash = shy + 128;                                       // [64]
     const int lane = threadIdx.x;
+    const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
     for (;;) {
         unsigned solve = 0;
         if (lane == 0) solve = atomicAdd(L.counter, 1u);
-        solve = __shfl(solve, 0, 64);
+        solve = __builtin_amdgcn_readfirstlane(__shfl(solve, 0, 64));
         if (solve >= (unsigned)L.nsolve) break;
         const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
         const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
         R *u = reinterpret_cast<R *>(L.u) + slot * L.field_elems;
         R *u0 = reinterpret_cast<R *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
-        const void *slow_model = SLOWMODE == 0
-            ? (const void *)(reinterpret_cast<const R *>(L.slow) + (size_t)model * L.field_elems)
-            : (const void *)(reinterpret_cast<const float *>(L.slow) + (size_t)model * L.ncx * L.ncy * L.ncz);
+        const void *slow_model;
+        uint32_t slow_bytes;
+        if (SLOWMODE == 0) {
+            slow_model = reinterpret_cast<const R *>(L.slow) + (size_t)model * L.field_elems;
+            slow_bytes = fbytes;
+        } else {
+            const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
+            slow_model = reinterpret_cast<const float *>(L.slow) + (size_t)model * ncell;
+            slow_bytes = (uint32_t)(ncell * 4);
+        }
+        const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
         BcBoxes bc;
         bc.box = bcbox;
-        const bool ok = init_field<R, SLOWMODE>(L, u, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
+        const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
         int iters = 0, ierr_last = 0;
         if (ok) {
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
@@ -433,9 +581,11 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
                     const bool first = sw == 0, last = sw == 7;
                     if (sw & 4)
-                        sweep<R, SLOWMODE, true>(L, u, u0, slow_model, bc, xh, rx, ry, first, last, notconv, ierr_last);
+                        sweep<R, SLOWMODE, true>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, rx, ry, first, last,
+                                                 notconv, ierr_last);
                     else
-                        sweep<R, SLOWMODE, false>(L, u, u0, slow_model, bc, xh, rx, ry, first, last, notconv, ierr_last);
+                        sweep<R, SLOWMODE, false>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, rx, ry, first, last,
+                                                  notconv, ierr_last);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
@@ -445,7 +595,7 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                 }
             }
         }
-        // reduce ierr over lanes (only the lane owning node (0,0,0) sets it)
+        // ierr: set only by the lane that owns node (0,0,0) in the last sweep
         int ierr = ierr_last;
         for (int o = 32; o > 0; o >>= 1) ierr = max(ierr, __shfl_xor(ierr, o, 64));
         if (!ok) ierr = 1;
@@ -506,7 +656,7 @@ int fsm_max_resident_waves(int dev, size_t lds_bytes, int is_double, int slow_mo
 template <typename R, int SLOWMODE>
 static hipError_t launch_fsm(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
-    size_t lds = BC_LDS_BYTES + (size_t)L.nzb * 8 * 8 * sizeof(R);
+    size_t lds = fsm_lds_bytes(L, sizeof(R));
     hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
 }
