@@ -324,13 +324,15 @@ class Sampler:
             pass
 
 
-def picks_from_forward(device=0):
-    """picks callable for make_problem: GPU forward (fp32) of the true model."""
+def picks_from_forward(device=0, precision=64):
+    """picks callable for make_problem: GPU forward of the true model (fp64 by
+    default: the reference's arithmetic, and a different kernel instance from
+    the fp32 sampler so profiles of the two do not mix)."""
     def f(p: Problem):
         import torch
         from .eikonal import BatchSolver
         dev = torch.device("cuda", device)
-        bs = BatchSolver(p.nx, p.ny, p.nz, p.h, p.x0, p.y0, p.z0, p.maxit, p.tol, 32, nref=p.nref)
+        bs = BatchSolver(p.nx, p.ny, p.nz, p.h, p.x0, p.y0, p.z0, p.maxit, p.tol, precision, nref=p.nref)
         src = torch.tensor(np.stack([np.zeros(p.nstat), p.sx, p.sy, p.sz], 1)[:, None, :], dtype=torch.float64)
         slow = torch.tensor((1.0 / p.v_true.astype(np.float32)).astype(np.float32).reshape(1, -1), device=dev)
         out = bs.solve(src, slow, ev_node=torch.tensor(p.ev_node))
