@@ -61,6 +61,8 @@ typedef struct mceik_fsm_batch {
     int *niter, *ierr;          /* device [nmodel*nstat] or NULL             */
     int max_sweeps;             /* < 0: unlimited (debug)                    */
     unsigned long long *iter_total;  /* device counter += iterations of every solve, or NULL */
+    int fast_sqrt;              /* 1: caller guarantees h*slowness >= 1e-12 (cells mode, fp32):
+                                   use the shorter correctly rounded sqrt (same results) */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */

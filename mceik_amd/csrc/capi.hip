@@ -18,7 +18,7 @@
 #include "mcmc_common.h"
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st);
-int fsm_occupancy(int is_double, int slow_mode, size_t lds);
+int fsm_occupancy(const FsmLaunch &L, int is_double);
 hipError_t fsm_to_brick_f64(const double *src, void *dst, int dst_double, const FsmLaunch &L, int nfield, hipStream_t st);
 hipError_t fsm_from_brick_f64(const void *src, int src_double, double *dst, const FsmLaunch &L, int nfield, hipStream_t st);
 hipError_t fsm_from_brick_f32(const float *src, float *dst, const FsmLaunch &L, int nfield, hipStream_t st);
@@ -77,6 +77,18 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.magic_ry = ((1u << 20) + L.nry - 1) / L.nry;
     L.magic_rz = ((1u << 20) + L.nrz - 1) / L.nrz;
     L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab;
+    // LDS cell cache when every tile's cells fit (2 x 2 x ncz at nref = 4)
+    {
+        auto span = [](int t, int n, int nr) {
+            int a = t * 8, e = t * 8 + 7 < n - 1 ? t * 8 + 7 : n - 1;
+            return e / nr - a / nr + 1;
+        };
+        int mx = 0, my = 0;
+        for (int t = 0; t < L.ntx; t++) { int v = span(t, L.nx, L.nrx); mx = v > mx ? v : mx; }
+        for (int t = 0; t < L.nty; t++) { int v = span(t, L.ny, L.nry); my = v > my ? v : my; }
+        L.cell_cache = b->slow_mode == 1 && mx * my * L.ncz <= 256 && L.nx < 4096 && L.ny < 4096 && L.nz < 4096;
+    }
+    L.fast_sqrt = b->fast_sqrt;
     L.niter = b->niter; L.ierr = b->ierr;
     L.iter_total = b->iter_total;
 }
@@ -99,15 +111,14 @@ static int device_cus()
 // Waves a launch keeps resident (one solve each): occupancy x CUs, at most nsolve.
 static int batch_waves(const FsmLaunch &L, int is_double)
 {
-    size_t lds = fsm_lds_bytes(L, is_double ? 8 : 4);
-    int per_cu = fsm_occupancy(is_double, L.slow_mode, lds);
+    int per_cu = fsm_occupancy(L, is_double);
     if (per_cu < 1) per_cu = 1;
     long w = (long)per_cu * device_cus();
     if (w > L.nsolve) w = L.nsolve;
     return (int)(w < 1 ? 1 : w);
 }
 
-// Workspace: [counter 256 B][slow brick copy (mode 0)][u scratch][u0 scratch]
+// Workspace: [8 queue heads, 1 KiB][slow brick copy (mode 0)][u scratch][u0 scratch]
 struct WsLayout {
     size_t counter, slow, u, u0, total;
     int nwaves;
@@ -122,7 +133,7 @@ static WsLayout ws_layout(const mceik_fsm_batch *b)
     WsLayout w;
     w.nwaves = batch_waves(L, is_double);
     w.counter = 0;
-    w.slow = 256;
+    w.slow = 1024;
     size_t slow_bytes = b->slow_mode == 0 ? (size_t)b->nmodel * L.field_elems * es : 0;
     w.u = w.slow + ((slow_bytes + 255) & ~(size_t)255);
     size_t nu = b->u_out ? (size_t)L.nsolve : (size_t)w.nwaves;
@@ -174,7 +185,7 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
     fill_launch(L, b);
     char *ws = (char *)workspace;
     L.counter = (unsigned *)(ws + w.counter);
-    HIPCHK(hipMemsetAsync(L.counter, 0, 256, st));
+    HIPCHK(hipMemsetAsync(L.counter, 0, 1024, st));
     if (b->slow_mode == 0) {
         void *sb = ws + w.slow;
         if (is_double)
@@ -536,6 +547,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = d_ierr;
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
+    b.fast_sqrt = parms->dx / (double)o->vmax >= 1e-12 ? 1 : 0;   // f = h/v stays a normal float
     s->ws_bytes = mceik_fsm_workspace_bytes(&b);
     if (hipMalloc(&s->ws, s->ws_bytes) != hipSuccess) {
         fprintf(stderr, "mceik_mcmc_init: cannot allocate %zu B of FSM workspace\n", s->ws_bytes);

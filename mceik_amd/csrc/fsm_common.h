@@ -32,7 +32,9 @@ struct FsmLaunch {
     float *ttab;                 // [nsolve][nev] travel times at events (fp32), may be null
     int *niter;                  // [nsolve] iterations executed, may be null
     int *ierr;                   // [nsolve] reference ierr semantics, may be null
-    unsigned *counter;           // work queue head (zeroed before the launch)
+    int cell_cache;              // slow_mode 1: every tile's cells fit the LDS cell cache
+    int fast_sqrt;               // host-validated: f = s*h is a normal float >= 1e-18
+    unsigned *counter;           // 8 work-queue heads, 128 B apart (zeroed before the launch)
     unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
 };
 
@@ -42,7 +44,9 @@ static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 // staged halos [8][8] + [8][2][8], lane trash [64]
 static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
 {
-    return (size_t)MCEIK_MAX_SRC * 6 * 4 + ((size_t)L.nzb * 64 + 512 + 64 + 128 + 64) * es;
+    const bool cached = L.slow_mode != 0 && L.cell_cache;
+    return (size_t)MCEIK_MAX_SRC * 6 * 4 + (cached ? 3 * 256 * 4 : 0) +
+           ((size_t)L.nzb * 64 + (cached ? 0 : 512) + 64 + 128 + 64) * es;
 }
 
 // Fills the tile geometry of a launch from nx, ny, nz.

@@ -175,9 +175,25 @@ __device__ __forceinline__ R shfl_up8(R v) { return __shfl_up(v, 8, 64); }
 template <typename R>
 __device__ __forceinline__ R shfl_down8(R v) { return __shfl_down(v, 8, 64); }
 
+// Correctly rounded sqrt for normal positive x (LLVM's expansion without the
+// denormal rescale and zero/inf fix-up).  Used only where the radicand that
+// is finally selected is provably a normal float: on the MCMC path f = h*s >=
+// h/vmax (checked on the host) and both radicands are then >= f^2 / 3.
+__device__ __forceinline__ float sqrt_normal(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __builtin_bit_cast(float, __builtin_bit_cast(int, s) - 1);
+    const float up = __builtin_bit_cast(float, __builtin_bit_cast(int, s) + 1);
+    const float edn = __builtin_fmaf(-dn, s, x);
+    const float eup = __builtin_fmaf(-up, s, x);
+    const float t = edn <= 0.0f ? dn : s;
+    return eup > 0.0f ? up : t;
+}
+
 // Branchless fp32 Godunov update (values and ierr identical to godunov(float)
 // above and to the twin): the 2D and 3D candidates are evaluated side by side,
 // so the two correctly rounded square roots are not serialised.
+template <bool FAST>
 __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, int &ierr)
 {
     const float UN = FLT_MAX;
@@ -185,11 +201,12 @@ __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, 
     const float a3 = fmaxf(fmaxf(a, b), c);
     const float a2 = __builtin_amdgcn_fmed3f(a, b, c);
     const float d2 = a2 - a1, d3 = a3 - a1;
-    const float y2 = 0.5f * (d2 + __builtin_sqrtf((2.0f * f) * f - d2 * d2));
+    const float r2 = (2.0f * f) * f - d2 * d2;
+    const float y2 = 0.5f * (d2 + (FAST ? sqrt_normal(r2) : __builtin_sqrtf(r2)));
     const float sm = d2 + d3;
     const float q = ((d2 * d2) + (d3 * d3)) - f * f;
     const float disc = sm * sm - 3.0f * q;
-    const float y3 = (sm + __builtin_sqrtf(disc)) * (1.0f / 3.0f);
+    const float y3 = (sm + (FAST ? sqrt_normal(disc) : __builtin_sqrtf(disc))) * (1.0f / 3.0f);
     const bool one = !(f > d2), two = !(y2 > d3);
     const float y = one ? f : (two ? y2 : y3);
     const float x = a1 + y;
@@ -198,6 +215,7 @@ __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, 
     ierr = nan_in ? 0 : (!ok ? 3 : ((!one && !two && disc < 0.0f) ? 1 : 0));
     return (nan_in || !ok) ? UN : x;
 }
+template <bool FAST>
 __device__ __forceinline__ double godunov_bl(double a, double b, double c, double f, int &ierr)
 {
     return godunov(a, b, c, f, ierr);   // fp64: the reference's literal form
@@ -221,7 +239,7 @@ struct BcBoxes {
 // Position of a lane in the tile/brick stream of one sweep, advanced by one
 // virtual brick per macro step (no divisions in the loop).
 struct Pos {
-    int vb, k, zbs, txs, tys;
+    int vb, k, zbs, txs, tys, k3;    // k3 = k mod 3 (cell-cache buffer of the tile)
 };
 
 __device__ __forceinline__ void pos_init(Pos &p, int vb, const FsmLaunch &L)
@@ -230,12 +248,14 @@ __device__ __forceinline__ void pos_init(Pos &p, int vb, const FsmLaunch &L)
     int v = vb < 0 ? 0 : vb;
     p.k = v / L.sb; p.zbs = v - p.k * L.sb;
     p.tys = p.k / L.ntx; p.txs = p.k - p.tys * L.ntx;
+    p.k3 = p.k % 3;
 }
 __device__ __forceinline__ void pos_adv(Pos &p, const FsmLaunch &L)
 {
     if (p.vb >= 0) {
         if (++p.zbs == L.sb) {
             p.zbs = 0; p.k++;
+            if (++p.k3 == 3) p.k3 = 0;
             if (++p.txs == L.ntx) { p.txs = 0; p.tys++; }
         }
     }
@@ -248,7 +268,18 @@ enum { F_VALID = 1, F_ACT = 2, F_XP = 4, F_XN = 8, F_YP = 16, F_YN = 32 };
 struct BInfo {
     uint32_t seg, hx, hy;    // byte offsets (u buffer): own segment, x-downwind halo, y halo (OOB if none)
     int zb8, flags, x, y;    // bits 8..15 of flags: BC z-slots (physical) of this column segment
+    int ccb;                 // cell-cache LDS index of this column's cell column (SLOWMODE 2)
 };
+
+#define CC_MAX 256           // floats per cell-cache buffer (3 buffers)
+
+// Cell range of a tile along one axis: first cell and count.
+__device__ __forceinline__ void tile_cells(int t, int n, unsigned magic, int &c0, int &nc)
+{
+    const int a = t * 8, b = min(t * 8 + 7, n - 1);
+    c0 = (int)(((unsigned)a * magic) >> 20);
+    nc = (int)(((unsigned)b * magic) >> 20) - c0 + 1;
+}
 
 template <typename R, bool RZ>
 __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Pos &p, int lx, int ly, int lxs, int lys,
@@ -291,6 +322,15 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Pos &p, in
         }
     }
     b.flags = fl | (int)(m << 8);
+    {
+        int cx0, ncxt, cy0, ncyt;
+        tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
+        tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
+        const int x = b.x < L.nx ? b.x : L.nx - 1, y = b.y < L.ny ? b.y : L.ny - 1;
+        const int cxl = (int)(((unsigned)x * L.magic_rx) >> 20) - cx0;
+        const int cyl = (int)(((unsigned)y * L.magic_ry) >> 20) - cy0;
+        b.ccb = valid ? p.k3 * CC_MAX + (cyl * ncxt + cxl) * L.ncz : 0;
+    }
     return b;
 }
 
@@ -298,7 +338,7 @@ template <typename R, int SLOWMODE>
 __device__ __forceinline__ double slow_at(const FsmLaunch &L, const void *slow_model, int x, int y, int z)
 {
     if (SLOWMODE == 0)
-        return (double)reinterpret_cast<const R *>(slow_model)[brick_index(L, x, y, z)];
+        return (double)reinterpret_cast<const R *>(slow_model)[brick_index(L, x, y, z)];   // modes 1, 2: cells
     const float *si = reinterpret_cast<const float *>(slow_model);
     return (double)si[((size_t)(z / L.nrz) * L.ncy + y / L.nry) * L.ncx + x / L.nrx];
 }
@@ -325,10 +365,43 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, Rsrc sr, const
     }
 }
 
+// Cell cache (SLOWMODE 2): the slowness cells a tile touches (2 x 2 x ncz at
+// nref = 4), three buffers indexed by tile ordinal mod 3.  Loads for tile kf
+// are issued one macro step before lane (0,0) enters it and written at the
+// end of that step; the buffer they replace (tile kf-3) has no reader left.
+__device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int kf, int rx, int ry, float (&v)[CC_MAX / 64],
+                                         int &size)
+{
+    const int lane = threadIdx.x;
+    const int tys = kf / L.ntx, txs = kf - tys * L.ntx;
+    const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+    int cx0, ncxt, cy0, ncyt;
+    tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
+    tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
+    size = kf < L.ntiles ? ncxt * ncyt * L.ncz : 0;
+#pragma unroll
+    for (int r = 0; r < CC_MAX / 64; r++) {
+        const int idx = lane + 64 * r;
+        const int cz = idx % L.ncz, t = idx / L.ncz;
+        const int cyl = t / ncxt, cxl = t - cyl * ncxt;
+        const uint32_t off = (uint32_t)(((cz * L.ncy + cy0 + cyl) * L.ncx) + cx0 + cxl) * 4u;
+        v[r] = bload1f(sr, idx < size ? off : OOB);
+    }
+}
+__device__ __forceinline__ void cc_write(float *cc, int buf, const float (&v)[CC_MAX / 64], int size)
+{
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < CC_MAX / 64; r++) {
+        const int idx = lane + 64 * r;
+        if (idx < size) cc[buf * CC_MAX + idx] = v[r];
+    }
+}
+
 // One Gauss-Seidel sweep over the whole grid in direction (rx, ry, RZ).
-template <typename R, int SLOWMODE, bool RZ>
+template <typename R, int SLOWMODE, bool FAST, bool RZ>
 __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
-                                      R *xh, R *sf, R *shx, R *shy, R *trash,
+                                      R *xh, R *sf, R *shx, R *shy, R *trash, float *cc,
                                       int rx, int ry, bool first_sweep, bool last_sweep,
                                       bool &notconv, int &ierr_last)
 {
@@ -340,12 +413,19 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
     const int hysel = lys >= 4;
 
     R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8];
+    float ccv[CC_MAX / 64];
+    int ccsize = 0, ccph = 1, cckf = 1, cck3 = 1;   // next fill: tile 1 at B = sb - 1
     Pos p1;
     pos_init(p1, -d, L);
     BInfo b0 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
     // prologue: c = brick(vb0), n = brick(vb0+1); stage f and halos of vb0
     bload8(ur, b0.seg, c);
-    prefetch_slow<R, SLOWMODE>(L, sr, b0, fq);
+    if (SLOWMODE == 2) {
+        cc_issue(L, sr, 0, rx, ry, ccv, ccsize);
+        cc_write(cc, 0, ccv, ccsize);
+    } else {
+        prefetch_slow<R, SLOWMODE>(L, sr, b0, fq);
+    }
     bload8(ur, b0.hx, hxq);
     bload8(ur, b0.hy, hyq);
     pos_adv(p1, L);
@@ -354,7 +434,10 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
         bload8(ur, b1.seg, n);
     }
 #pragma unroll
-    for (int i = 0; i < 8; i++) { r[i] = UN; sf[i * 64 + lane] = fq[i] * hr; }
+    for (int i = 0; i < 8; i++) {
+        r[i] = UN;
+        if (SLOWMODE != 2) sf[i * 64 + lane] = fq[i] * hr;
+    }
     if (lxs == 7) {
 #pragma unroll
         for (int i = 0; i < 8; i++) shx[i * 8 + lys] = hxq[i];
@@ -380,7 +463,13 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
             }
             bload8(ur, seg2, q);
         }
-        prefetch_slow<R, SLOWMODE>(L, sr, b1, fq);
+        bool ccfill = false;
+        if (SLOWMODE == 2) {
+            ccfill = ccph == 0;                  // B + 1 == cckf * sb: lane (0,0) enters tile cckf next step
+            if (ccfill) cc_issue(L, sr, cckf, rx, ry, ccv, ccsize);
+        } else {
+            prefetch_slow<R, SLOWMODE>(L, sr, b1, fq);
+        }
         bload8(ur, b1.hx, hxq);
         bload8(ur, b1.hy, hyq);
 
@@ -397,7 +486,11 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
             const R self = c[pj];
             const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
             const R ym = shfl_up8(r[pj]), ypv = shfl_down8(n[pj]);
-            const R fv = sf[pj * 64 + lane];
+            R fv;
+            if (SLOWMODE == 2)
+                fv = (R)cc[b0.ccb + (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20)] * hr;
+            else
+                fv = sf[pj * 64 + lane];
             const R hxv = shx[pj * 8 + lys];
             const R hyv = shy[(pj * 2 + hysel) * 8 + lxs];
             const R xhv = xh[zabs * 8 + lys];
@@ -413,7 +506,7 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
             const R uy = yup < ydn ? yup : ydn;
             const R uz = zup < zdn ? zup : zdn;
             int e;
-            const R ub = godunov_bl(ux, uy, uz, fv, e);
+            const R ub = godunov_bl<FAST>(ux, uy, uz, fv, e);
             const bool upd = act && zabs < L.nz && !((fl >> (8 + pj)) & 1);
             const R nv = upd ? (self < ub ? self : ub) : self;
             if (upd && nv < self && self >= T) notconv = true;
@@ -452,8 +545,17 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
         }
         asm volatile("" ::: "memory");
         // ---- stage the prefetched slowness/halos of vb+1 for the next step
+        if (SLOWMODE == 2) {
+            if (ccfill) {
+                cc_write(cc, cck3, ccv, ccsize);
+                cckf++;
+                if (++cck3 == 3) cck3 = 0;
+            }
+            if (++ccph == L.sb) ccph = 0;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 8; i++) sf[i * 64 + lane] = fq[i] * hr;
+            for (int i = 0; i < 8; i++) sf[i * 64 + lane] = fq[i] * hr;
+        }
         if (lxs == 7) {
 #pragma unroll
             for (int i = 0; i < 8; i++) shx[i * 8 + lys] = hxq[i];
@@ -537,23 +639,43 @@ __device__ bool init_field(const FsmLaunch &L, R *u, Rsrc ur, const void *slow_m
     return ok;
 }
 
-template <typename R, int SLOWMODE>
+// Work queue: 8 groups (blockIdx % 8, which the dispatcher deals round-robin
+// over the XCDs -- speed only, never correctness); group g first drains the
+// contiguous solve range [g*S/8, (g+1)*S/8) -- consecutive solves share a model,
+// so a model's cells stay in one XCD's L2 -- then steals from the others.
+__device__ __forceinline__ int next_solve(const FsmLaunch &L, int &pass)
+{
+    const int g0 = blockIdx.x & 7;
+    while (pass < 8) {
+        const int g = (g0 + pass) & 7;
+        const int lo = (int)((long long)L.nsolve * g / 8), hi = (int)((long long)L.nsolve * (g + 1) / 8);
+        unsigned i = 0;
+        if (threadIdx.x == 0) i = atomicAdd(L.counter + 32 * g, 1u);
+        i = __builtin_amdgcn_readfirstlane(__shfl(i, 0, 64));
+        if ((int)i < hi - lo) return lo + (int)i;
+        pass++;
+    }
+    return -1;
+}
+
+template <typename R, int SLOWMODE, bool FAST>
 __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int *bcbox = reinterpret_cast<int *>(smem);                 // 192 B, 16-B multiple
-    R *xh = reinterpret_cast<R *>(smem + BC_LDS_BYTES);         // [nzb*8][8]
+    float *cc = reinterpret_cast<float *>(smem + BC_LDS_BYTES); // [3][CC_MAX] cell cache (SLOWMODE 2)
+    R *xh = reinterpret_cast<R *>(smem + BC_LDS_BYTES + (SLOWMODE == 2 ? 3 * CC_MAX * 4 : 0));   // [nzb*8][8]
     R *sf = xh + (size_t)L.nzb * 64;                            // [8][64] staged f = s*h
-    R *shx = sf + 512;                                          // [8][8]   x-downwind halo
+    R *shx = sf + (SLOWMODE == 2 ? 0 : 512);                    // [8][8]   x-downwind halo
     R *shy = shx + 64;                                          // [8][2][8] y halos
     R *trash = shy + 128;                                       // [64]
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
+    int pass = 0;
     for (;;) {
-        unsigned solve = 0;
-        if (lane == 0) solve = atomicAdd(L.counter, 1u);
-        solve = __builtin_amdgcn_readfirstlane(__shfl(solve, 0, 64));
-        if (solve >= (unsigned)L.nsolve) break;
+        const int snext = next_solve(L, pass);
+        if (snext < 0) break;
+        const unsigned solve = (unsigned)snext;
         const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
         const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
         R *u = reinterpret_cast<R *>(L.u) + slot * L.field_elems;
@@ -581,11 +703,11 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
                     const bool first = sw == 0, last = sw == 7;
                     if (sw & 4)
-                        sweep<R, SLOWMODE, true>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, rx, ry, first, last,
-                                                 notconv, ierr_last);
+                        sweep<R, SLOWMODE, FAST, true>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, cc, rx, ry,
+                                                       first, last, notconv, ierr_last);
                     else
-                        sweep<R, SLOWMODE, false>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, rx, ry, first, last,
-                                                  notconv, ierr_last);
+                        sweep<R, SLOWMODE, FAST, false>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, cc, rx, ry,
+                                                        first, last, notconv, ierr_last);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
@@ -651,33 +773,54 @@ __global__ void from_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfiel
 }  // namespace
 
 // ---- host-side launchers (C++ linkage, used by capi.hip) ---------------------
-int fsm_max_resident_waves(int dev, size_t lds_bytes, int is_double, int slow_mode);
-
-template <typename R, int SLOWMODE>
+template <typename R, int SLOWMODE, bool FAST>
 static hipError_t launch_fsm(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     size_t lds = fsm_lds_bytes(L, sizeof(R));
-    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE>), dim3(nwaves), dim3(64), lds, st, L);
+    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
+}
+
+template <typename R, int SLOWMODE, bool FAST>
+static int occupancy_of(size_t lds)
+{
+    int nb = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST>, 64, lds) == hipSuccess
+        ? nb : 1;
+}
+
+// Kernel variant of a launch: slowness source and sqrt form.
+static int variant(const FsmLaunch &L, int is_double)
+{
+    int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
+    return mode * 2 + (!is_double && mode == 2 && L.fast_sqrt ? 1 : 0);
 }
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st)
 {
-    if (is_double) return L.slow_mode ? launch_fsm<double, 1>(L, nwaves, st) : launch_fsm<double, 0>(L, nwaves, st);
-    return L.slow_mode ? launch_fsm<float, 1>(L, nwaves, st) : launch_fsm<float, 0>(L, nwaves, st);
+    switch (variant(L, is_double) + (is_double ? 8 : 0)) {
+    case 0: return launch_fsm<float, 0, false>(L, nwaves, st);
+    case 2: return launch_fsm<float, 1, false>(L, nwaves, st);
+    case 4: return launch_fsm<float, 2, false>(L, nwaves, st);
+    case 5: return launch_fsm<float, 2, true>(L, nwaves, st);
+    case 8: return launch_fsm<double, 0, false>(L, nwaves, st);
+    case 10: return launch_fsm<double, 1, false>(L, nwaves, st);
+    default: return launch_fsm<double, 2, false>(L, nwaves, st);
+    }
 }
 
-int fsm_occupancy(int is_double, int slow_mode, size_t lds)
+int fsm_occupancy(const FsmLaunch &L, int is_double)
 {
-    int nb = 0;
-    hipError_t e;
-    if (is_double)
-        e = slow_mode ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<double, 1>, 64, lds)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<double, 0>, 64, lds);
-    else
-        e = slow_mode ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<float, 1>, 64, lds)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<float, 0>, 64, lds);
-    return e == hipSuccess ? nb : 1;
+    const size_t lds = fsm_lds_bytes(L, is_double ? 8 : 4);
+    switch (variant(L, is_double) + (is_double ? 8 : 0)) {
+    case 0: return occupancy_of<float, 0, false>(lds);
+    case 2: return occupancy_of<float, 1, false>(lds);
+    case 4: return occupancy_of<float, 2, false>(lds);
+    case 5: return occupancy_of<float, 2, true>(lds);
+    case 8: return occupancy_of<double, 0, false>(lds);
+    case 10: return occupancy_of<double, 1, false>(lds);
+    default: return occupancy_of<double, 2, false>(lds);
+    }
 }
 
 hipError_t fsm_to_brick_f64(const double *src, void *dst, int dst_double, const FsmLaunch &L, int nfield, hipStream_t st)
