@@ -1,0 +1,91 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares, and
+the data-model structs are ABI-identical to the reference's mceik_struct.h.
+No compute calls (no GPU needed)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+REF_INC = "/root/reference/include"
+
+
+def _declared_functions():
+    names = set()
+    for h in ("mceik.h", "mceik_eikonal.h"):
+        txt = open(os.path.join(INC, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:int|void|size_t|double)\s+\**\s*([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from mceik_amd import _lib
+    L = _lib.lib()
+    declared = _declared_functions()
+    assert len(declared) >= 14
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    for name in declared:
+        assert name in exported, name
+        assert getattr(L, name) is not None
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    from mceik_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libmceik_hip.so")
+    with pytest.raises(ImportError):
+        _lib.lib()
+
+
+LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "mceik_struct.h"
+#define P(T, m) printf(#T "." #m " %zu\n", offsetof(struct T, m))
+int main(void) {
+  printf("catalog %zu stations %zu mcmc %zu eik %zu parms %zu\n", sizeof(struct mceik_catalog_struct),
+         sizeof(struct mceik_stations_struct), sizeof(struct mcmc_parms_struct), sizeof(struct eik_parms_struct),
+         sizeof(struct mceik_parms_struct));
+  P(mceik_catalog_struct, xsrc); P(mceik_catalog_struct, varObs); P(mceik_catalog_struct, obsPtr);
+  P(mceik_catalog_struct, nevents); P(mceik_stations_struct, xrec); P(mceik_stations_struct, lhasS);
+  P(mceik_stations_struct, nstat); P(mceik_stations_struct, lcartesian); P(mcmc_parms_struct, keepK);
+  P(mceik_parms_struct, eikparms); P(mceik_parms_struct, projnm); P(mceik_parms_struct, x0);
+  P(mceik_parms_struct, dz); P(mceik_parms_struct, ndivz); P(mceik_parms_struct, nrefz);
+  printf("P %d S %d\n", P_PRIMARY_PICK, S_PRIMARY_PICK);
+  return 0;
+}
+"""
+
+
+def _layout(incdir):
+    with tempfile.TemporaryDirectory() as td:
+        src = os.path.join(td, "l.c")
+        open(src, "w").write(LAYOUT_C)
+        exe = os.path.join(td, "l")
+        subprocess.run(["gcc", "-I", incdir, src, "-o", exe], check=True)
+        return subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_INC), reason="reference headers not present (GPU box)")
+def test_struct_layout_identical_to_reference_header():
+    assert _layout(INC) == _layout(REF_INC)
+
+
+def test_ctypes_mirrors_match_header():
+    from mceik_amd import _lib
+    out = _layout(INC).split()
+    sizes = dict(zip(out[0:10:2], map(int, out[1:10:2])))
+    assert C.sizeof(_lib.CatalogStruct) == sizes["catalog"]
+    assert C.sizeof(_lib.StationsStruct) == sizes["stations"]
+    assert C.sizeof(_lib.McmcParms) == sizes["mcmc"]
+    assert C.sizeof(_lib.EikParms) == sizes["eik"]
+    assert C.sizeof(_lib.MceikParms) == sizes["parms"]
+    assert _lib.MceikParms.nrefz.offset == int(_layout(INC).split("mceik_parms_struct.nrefz ")[1].split()[0])
