@@ -22,7 +22,8 @@ class FsmBatch(C.Structure):
                 ("nrx", C.c_int), ("nry", C.c_int), ("nrz", C.c_int),
                 ("nev", C.c_int), ("ev_node", C.c_void_p), ("ttab", C.c_void_p),
                 ("u_out", C.c_void_p), ("niter", C.c_void_p), ("ierr", C.c_void_p),
-                ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int)]
+                ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
+                ("tile_total", C.c_void_p)]
 
 
 class McmcParms(C.Structure):
@@ -114,7 +115,7 @@ def lib():
     L.mceik_mcmc_last.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 3
     L.mceik_mcmc_fsm_stats.restype = C.c_int
     L.mceik_mcmc_fsm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong),
-                                       C.POINTER(C.c_ulonglong), C.c_int]
+                                       C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]
     L.mceik_mcmc_finalize.restype = C.c_int
     L.mceik_mcmc_finalize.argtypes = [C.POINTER(C.c_void_p)]
     _lib = L

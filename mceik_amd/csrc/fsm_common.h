@@ -4,6 +4,7 @@
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
+#include <hip/hip_runtime.h>
 
 #define MCEIK_MAX_SRC 8          // point sources per solve (box BCs, fsm3d.f90:762-840)
 #define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
@@ -36,18 +37,42 @@ struct FsmLaunch {
     int fast_sqrt;               // host-validated: f = s*h is a normal float >= 1e-18
     unsigned *counter;           // 8 work-queue heads, 128 B apart (zeroed before the launch)
     unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
+    unsigned long long *tile_total;   // += tile visits (one tile x nzb bricks, one sweep), may be null
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 
-// LDS of one solve wave: BC boxes, x halo column [nzb*8][8], staged f [8][64],
-// staged halos [8][8] + [8][2][8], lane trash [64]
-static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
+// LDS of one solve wave (byte offsets, shared by host and device):
+//  0 BC boxes [MAX_SRC][6] int | 1 cell cache [3][256] float (cached mode) |
+//  2 diagonal tile order int | 3 lastproc int | 4 lastchg int | 5 u0 epoch u16 |
+//  6 small-change epoch u16 (all [ntiles]) | 7 stream ring [4] int |
+//  8 staged f [8][64] R (uncached) | 9 x halos [8][2][8] R | 10 y halos [8][2][8] R
+#define MCEIK_CC_MAX 256
+static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
+static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, size_t es, size_t *off)
 {
     const bool cached = L.slow_mode != 0 && L.cell_cache;
-    return (size_t)MCEIK_MAX_SRC * 6 * 4 + (cached ? 3 * 256 * 4 : 0) +
-           ((size_t)L.nzb * 64 + (cached ? 0 : 512) + 64 + 128 + 64) * es;
+    const size_t nt = (size_t)L.ntiles;
+    size_t o = 0;
+    off[0] = o; o += mceik_align16(MCEIK_MAX_SRC * 6 * 4);
+    off[1] = o; o += cached ? 3 * MCEIK_CC_MAX * 4 : 0;
+    off[2] = o; o += mceik_align16(nt * 4);
+    off[3] = o; o += mceik_align16(nt * 4);
+    off[4] = o; o += mceik_align16(nt * 4);
+    off[5] = o; o += mceik_align16(nt * 2);
+    off[6] = o; o += mceik_align16(nt * 2);
+    off[7] = o; o += 16;
+    off[8] = o; o += cached ? 0 : 512 * es;
+    off[9] = o; o += 128 * es;
+    off[10] = o; o += 128 * es;
+    return o;
 }
+static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
+{
+    size_t off[11];
+    return fsm_smem_layout(L, es, off);
+}
+#define MCEIK_MAX_LDS (64 * 1024)   // dynamic LDS without a launch attribute
 
 // Fills the tile geometry of a launch from nx, ny, nz.
 static inline void fsm_geometry(FsmLaunch *L)

@@ -234,44 +234,76 @@ struct BcBoxes {
     int n;
     int *box;          // LDS, [MCEIK_MAX_SRC][6]
 };
-#define BC_LDS_BYTES (MCEIK_MAX_SRC * 6 * 4)
 
-// Position of a lane in the tile/brick stream of one sweep, advanced by one
-// virtual brick per macro step (no divisions in the loop).
-struct Pos {
-    int vb, k, zbs, txs, tys, k3;    // k3 = k mod 3 (cell-cache buffer of the tile)
+// ---- LDS working set of one solve wave -------------------------------------
+// Tiles are streamed through the wave in diagonal (wavefront) order of the
+// sweep direction; a tile enters the stream only if it or a face neighbour
+// changed since its last visit (exact: an update of unchanged inputs returns
+// the node's current value).  Per-tile clocks live in LDS.
+template <typename R>
+struct Smem {
+    int *box;                    // BC boxes [MCEIK_MAX_SRC][6]
+    float *cc;                   // cell cache [3][CC_MAX]            (SLOWMODE 2)
+    int *order;                  // diagonal order: txs | tys << 16   [ntiles]
+    int *lastproc, *lastchg;     // stream clock of the last visit / last visit with a change
+    unsigned short *u0ep;        // iteration+1 of the last u0 store of the tile
+    unsigned short *smallit;     // iteration+1 of the last change of a node below T
+    int *ring;                   // stream entries of positions p & 3: tx | ty << 12 | u0 flag << 24
+    R *sf, *shx, *shy;           // staged slowness*h (modes 0,1) and halos
 };
 
-__device__ __forceinline__ void pos_init(Pos &p, int vb, const FsmLaunch &L)
+#define CC_MAX MCEIK_CC_MAX      // floats per cell-cache buffer (3 buffers)
+
+template <typename R>
+__device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *base)
+{
+    size_t off[11];
+    fsm_smem_layout(L, sizeof(R), off);
+    Smem<R> S;
+    S.box = reinterpret_cast<int *>(base + off[0]);
+    S.cc = reinterpret_cast<float *>(base + off[1]);
+    S.order = reinterpret_cast<int *>(base + off[2]);
+    S.lastproc = reinterpret_cast<int *>(base + off[3]);
+    S.lastchg = reinterpret_cast<int *>(base + off[4]);
+    S.u0ep = reinterpret_cast<unsigned short *>(base + off[5]);
+    S.smallit = reinterpret_cast<unsigned short *>(base + off[6]);
+    S.ring = reinterpret_cast<int *>(base + off[7]);
+    S.sf = reinterpret_cast<R *>(base + off[8]);
+    S.shx = reinterpret_cast<R *>(base + off[9]);
+    S.shy = reinterpret_cast<R *>(base + off[10]);
+    return S;
+}
+
+// Position of a lane in the stream of one sweep: stream position sp (tile
+// ordinal within the sweep) and z-brick zbs, advanced one virtual brick per
+// macro step.  sp3 = sp mod 3 selects the cell-cache buffer.
+struct Pos {
+    int vb, sp, zbs, sp3;
+};
+__device__ __forceinline__ void pos_init(Pos &p, int vb, int sb)
 {
     p.vb = vb;
-    int v = vb < 0 ? 0 : vb;
-    p.k = v / L.sb; p.zbs = v - p.k * L.sb;
-    p.tys = p.k / L.ntx; p.txs = p.k - p.tys * L.ntx;
-    p.k3 = p.k % 3;
+    const int v = vb < 0 ? 0 : vb;
+    p.sp = v / sb; p.zbs = v - p.sp * sb; p.sp3 = p.sp % 3;
 }
-__device__ __forceinline__ void pos_adv(Pos &p, const FsmLaunch &L)
+__device__ __forceinline__ void pos_adv(Pos &p, int sb)
 {
-    if (p.vb >= 0) {
-        if (++p.zbs == L.sb) {
-            p.zbs = 0; p.k++;
-            if (++p.k3 == 3) p.k3 = 0;
-            if (++p.txs == L.ntx) { p.txs = 0; p.tys++; }
-        }
+    if (p.vb >= 0 && ++p.zbs == sb) {
+        p.zbs = 0; p.sp++;
+        if (++p.sp3 == 3) p.sp3 = 0;
     }
     p.vb++;
 }
 
-enum { F_VALID = 1, F_ACT = 2, F_XP = 4, F_XN = 8, F_YP = 16, F_YN = 32 };
+enum { F_VALID = 1, F_ACT = 2, F_XP = 4, F_XN = 8, F_YP = 16, F_YN = 32, F_U0 = 64 };
 
 // What a lane needs about one of its bricks.
 struct BInfo {
-    uint32_t seg, hx, hy;    // byte offsets (u buffer): own segment, x-downwind halo, y halo (OOB if none)
+    uint32_t seg, hx, hy;    // byte offsets (u buffer): own segment, x halo, y halo (OOB if none)
     int zb8, flags, x, y;    // bits 8..15 of flags: BC z-slots (physical) of this column segment
     int ccb;                 // cell-cache LDS index of this column's cell column (SLOWMODE 2)
+    int sp;                  // stream position (sweep-local) of the brick's tile
 };
-
-#define CC_MAX 256           // floats per cell-cache buffer (3 buffers)
 
 // Cell range of a tile along one axis: first cell and count.
 __device__ __forceinline__ void tile_cells(int t, int n, unsigned magic, int &c0, int &nc)
@@ -281,34 +313,45 @@ __device__ __forceinline__ void tile_cells(int t, int n, unsigned magic, int &c0
     nc = (int)(((unsigned)b * magic) >> 20) - c0 + 1;
 }
 
+__device__ __forceinline__ bool pos_valid(const Pos &p, int nstream, int nzb)
+{
+    return p.vb >= 0 && p.sp < nstream && p.zbs < nzb;
+}
+
 template <typename R, bool RZ>
-__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Pos &p, int lx, int ly, int lxs, int lys,
-                                            int rx, int ry, const BcBoxes &bc)
+__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
+                                            int lx, int ly, int lxs, int lys, int rx, int ry, const BcBoxes &bc)
 {
     BInfo b;
-    const bool valid = p.vb >= 0 && p.k < L.ntiles && p.zbs < L.nzb;
-    int tx = rx ? L.ntx - 1 - p.txs : p.txs, ty = ry ? L.nty - 1 - p.tys : p.tys;
-    int zb = RZ ? L.nzb - 1 - p.zbs : p.zbs;
-    if (!valid) { tx = 0; ty = 0; zb = 0; }
+    const bool valid = pos_valid(p, nstream, L.nzb);
+    const int e = valid ? S.ring[p.sp & 3] : 0;
+    const int tx = e & 0xfff, ty = (e >> 12) & 0xfff;
+    const int zb = valid ? (RZ ? L.nzb - 1 - p.zbs : p.zbs) : 0;
+    b.sp = p.sp;
     b.zb8 = zb * 8;
     b.x = tx * 8 + lx; b.y = ty * 8 + ly;
     const bool inxy = b.x < L.nx && b.y < L.ny;
     const bool xlo = b.x > 0, xhi = b.x < L.nx - 1, ylo = b.y > 0, yhi = b.y < L.ny - 1;
     const bool xp = rx ? xhi : xlo, xn = rx ? xlo : xhi, yp = ry ? yhi : ylo, yn = ry ? ylo : yhi;
     int fl = (valid ? F_VALID : 0) | ((valid && inxy) ? F_ACT : 0) | (xp ? F_XP : 0) | (xn ? F_XN : 0) |
-             (yp ? F_YP : 0) | (yn ? F_YN : 0);
+             (yp ? F_YP : 0) | (yn ? F_YN : 0) | ((valid && ((e >> 24) & 1)) ? F_U0 : 0);
     const uint32_t es = sizeof(R);
     const uint32_t stride_tile = (uint32_t)L.nzb * 512u;
     b.seg = valid ? ((uint32_t)(ty * L.ntx + tx) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lx) * 8u) * es : OOB;
+    // x halo: lane lx'=0 takes the sweep-upwind column (new values, from HBM),
+    // lane lx'=7 the sweep-downwind column of the next tile (old values)
     b.hx = OOB;
-    if (valid && lxs == 7 && xn) {
-        int txn = rx ? tx - 1 : tx + 1, lxn = rx ? 7 : 0;
-        b.hx = ((uint32_t)(ty * L.ntx + txn) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lxn) * 8u) * es;
+    if (valid && ((lxs == 0 && xp) || (lxs == 7 && xn))) {
+        const bool up = lxs == 0;
+        const int txh = (up != (rx != 0)) ? tx - 1 : tx + 1;
+        const int lxh = (up != (rx != 0)) ? 7 : 0;
+        b.hx = ((uint32_t)(ty * L.ntx + txh) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lxh) * 8u) * es;
     }
     b.hy = OOB;
     if (valid && ((lys == 0 && yp) || (lys == 7 && yn))) {
-        int tyh = (lys == 0) == (ry == 0) ? ty - 1 : ty + 1;
-        int lyh = (lys == 0) == (ry == 0) ? 7 : 0;
+        const bool up = lys == 0;
+        const int tyh = (up != (ry != 0)) ? ty - 1 : ty + 1;
+        const int lyh = (up != (ry != 0)) ? 7 : 0;
         b.hy = ((uint32_t)(tyh * L.ntx + tx) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(lyh * 8 + lx) * 8u) * es;
     }
     // BC z-slots of this column segment
@@ -329,7 +372,7 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Pos &p, in
         const int x = b.x < L.nx ? b.x : L.nx - 1, y = b.y < L.ny ? b.y : L.ny - 1;
         const int cxl = (int)(((unsigned)x * L.magic_rx) >> 20) - cx0;
         const int cyl = (int)(((unsigned)y * L.magic_ry) >> 20) - cy0;
-        b.ccb = valid ? p.k3 * CC_MAX + (cyl * ncxt + cxl) * L.ncz : 0;
+        b.ccb = valid ? p.sp3 * CC_MAX + (cyl * ncxt + cxl) * L.ncz : 0;
     }
     return b;
 }
@@ -366,19 +409,18 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, Rsrc sr, const
 }
 
 // Cell cache (SLOWMODE 2): the slowness cells a tile touches (2 x 2 x ncz at
-// nref = 4), three buffers indexed by tile ordinal mod 3.  Loads for tile kf
-// are issued one macro step before lane (0,0) enters it and written at the
-// end of that step; the buffer they replace (tile kf-3) has no reader left.
-__device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int kf, int rx, int ry, float (&v)[CC_MAX / 64],
-                                         int &size)
+// nref = 4), three buffers indexed by stream position mod 3.  Loads for the
+// tile at position k are issued one macro step before lane (0,0) enters it and
+// written at the end of that step; the buffer they replace (position k-3) has
+// no reader left (sb >= 11).
+__device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int entry, float (&v)[CC_MAX / 64], int &size)
 {
     const int lane = threadIdx.x;
-    const int tys = kf / L.ntx, txs = kf - tys * L.ntx;
-    const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
     int cx0, ncxt, cy0, ncyt;
     tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
     tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
-    size = kf < L.ntiles ? ncxt * ncyt * L.ncz : 0;
+    size = entry >= 0 ? ncxt * ncyt * L.ncz : 0;
 #pragma unroll
     for (int r = 0; r < CC_MAX / 64; r++) {
         const int idx = lane + 64 * r;
@@ -398,85 +440,170 @@ __device__ __forceinline__ void cc_write(float *cc, int buf, const float (&v)[CC
     }
 }
 
-// One Gauss-Seidel sweep over the whole grid in direction (rx, ry, RZ).
+// Choose the next tile of the stream: the first tile (diagonal order from
+// `cursor`) that changed at its last visit, has a face neighbour that changed
+// since, or has a sweep-upwind neighbour still in flight (whose changes are
+// not known yet).  64 candidates are judged per ballot.  Returns the ring
+// entry (tx | ty << 12) or -1 when the sweep has no tile left.
+template <typename R>
+__device__ int choose_tile(const FsmLaunch &L, const Smem<R> &S, int &cursor, int infl0, int infl1, int rx, int ry)
+{
+    const int lane = threadIdx.x;
+    while (cursor < L.ntiles) {
+        const int k = cursor + lane;
+        bool dirty = false;
+        int entry = 0;
+        if (k < L.ntiles) {
+            const int o = S.order[k];
+            const int txs = o & 0xffff, tys = o >> 16;
+            const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+            const int id = ty * L.ntx + tx;
+            const int lp = S.lastproc[id];
+            dirty = S.lastchg[id] >= lp;
+            if (tx > 0) dirty |= S.lastchg[id - 1] > lp;
+            if (tx < L.ntx - 1) dirty |= S.lastchg[id + 1] > lp;
+            if (ty > 0) dirty |= S.lastchg[id - L.ntx] > lp;
+            if (ty < L.nty - 1) dirty |= S.lastchg[id + L.ntx] > lp;
+            const int xu = txs > 0 ? id + (rx ? 1 : -1) : -2;
+            const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -2;
+            dirty |= xu == infl0 || xu == infl1 || yu == infl0 || yu == infl1;
+            entry = tx | (ty << 12);
+        }
+        const unsigned long long m = __ballot(dirty);
+        if (m) {
+            const int first = __builtin_ctzll(m);
+            cursor += first + 1;
+            return __shfl(entry, first, 64);
+        }
+        cursor += 64;
+    }
+    return -1;
+}
+
+// Admit the chosen tile at stream position pos (all lanes call; lane 0 writes).
+template <typename R>
+__device__ __forceinline__ void admit_tile(const FsmLaunch &L, const Smem<R> &S, int entry, int pos, int clock, int it)
+{
+    const int id = (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
+    const int u0flag = S.u0ep[id] != (unsigned short)(it + 1);
+    asm volatile("" ::: "memory");
+    if (threadIdx.x == 0) {
+        S.u0ep[id] = (unsigned short)(it + 1);
+        S.lastproc[id] = clock;
+        S.ring[pos & 3] = entry | (u0flag << 24);
+    }
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int ring_tile(const FsmLaunch &L, const int *ring, int pos)
+{
+    if (pos < 0) return -1;
+    const int e = ring[pos & 3];
+    return (e & 0xfff) + ((e >> 12) & 0xfff) * L.ntx;
+}
+
+// One Gauss-Seidel sweep over the grid in direction (rx, ry, RZ): only the
+// tiles admitted by choose_tile are visited.  Returns the number of stream
+// positions used (the clock advance).
 template <typename R, int SLOWMODE, bool FAST, bool RZ>
-__device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
-                                      R *xh, R *sf, R *shx, R *shy, R *trash, float *cc,
-                                      int rx, int ry, bool first_sweep, bool last_sweep,
-                                      bool &notconv, int &ierr_last)
+__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
+                                     const Smem<R> &S, int rx, int ry, int it, int clock0,
+                                     bool &notconv, int &ierr_last, unsigned long long &visited)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
-    const R hr = (R)L.h, T = (R)L.conv_thresh, tolr = (R)L.tol;
-    const int nmacro = L.ntiles * L.sb + 14;
-    const int hysel = lys >= 4;
+    const R hr = (R)L.h, T = (R)L.conv_thresh;
+    const int sb = L.sb;
+    const int hxsel = lxs == 7, hysel = lys >= 4;
 
+    // stream bookkeeping (wave-uniform)
+    int cursor = 0, ndecided = 0, nstream = 0x7fffffff;
+    {
+        const int e = choose_tile<R>(L, S, cursor, -1, -1, rx, ry);
+        if (e < 0) return 0;                                // nothing changed near any tile: skip the sweep
+        admit_tile<R>(L, S, e, 0, clock0, it);
+        ndecided = 1;
+    }
     R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8];
     float ccv[CC_MAX / 64];
-    int ccsize = 0, ccph = 1, cckf = 1, cck3 = 1;   // next fill: tile 1 at B = sb - 1
+    int ccsize = 0;
     Pos p1;
-    pos_init(p1, -d, L);
-    BInfo b0 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
+    pos_init(p1, -d, sb);
+    BInfo b0 = brick_info<R, RZ>(L, S, p1, nstream, lx, ly, lxs, lys, rx, ry, bc);
     // prologue: c = brick(vb0), n = brick(vb0+1); stage f and halos of vb0
     bload8(ur, b0.seg, c);
     if (SLOWMODE == 2) {
-        cc_issue(L, sr, 0, rx, ry, ccv, ccsize);
-        cc_write(cc, 0, ccv, ccsize);
+        cc_issue(L, sr, S.ring[0] & 0xffffff, ccv, ccsize);
+        cc_write(S.cc, 0, ccv, ccsize);
     } else {
         prefetch_slow<R, SLOWMODE>(L, sr, b0, fq);
     }
     bload8(ur, b0.hx, hxq);
     bload8(ur, b0.hy, hyq);
-    pos_adv(p1, L);
+    pos_adv(p1, sb);
     {
-        BInfo b1 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
+        BInfo b1 = brick_info<R, RZ>(L, S, p1, nstream, lx, ly, lxs, lys, rx, ry, bc);
         bload8(ur, b1.seg, n);
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         r[i] = UN;
-        if (SLOWMODE != 2) sf[i * 64 + lane] = fq[i] * hr;
+        if (SLOWMODE != 2) S.sf[i * 64 + lane] = fq[i] * hr;
     }
-    if (lxs == 7) {
+    if (lxs == 0 || lxs == 7) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) shx[i * 8 + lys] = hxq[i];
+        for (int i = 0; i < 8; i++) S.shx[(i * 2 + hxsel) * 8 + lys] = hxq[i];
     }
     if (lys == 0 || lys == 7) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
+        for (int i = 0; i < 8; i++) S.shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
     }
+    asm volatile("" ::: "memory");
 
-    for (int B = 0; B < nmacro; B++) {
+    int ph = 2 % sb;                 // (B + 2) mod sb: 0 when lane (0,0)'s vb+2 starts a new position
+    for (int B = 0; B < (nstream == 0x7fffffff ? 0x7fffffff : nstream * sb + 14); B++) {
+        // ---- stream decision for the position lane (0,0) prefetches next
+        bool ccfill = false;
+        if (ph == 0 && nstream == 0x7fffffff) {
+            const int pos = ndecided;
+            const int e = choose_tile<R>(L, S, cursor, ring_tile(L, S.ring, pos - 1), ring_tile(L, S.ring, pos - 2),
+                                         rx, ry);
+            if (e < 0) {
+                nstream = pos;
+            } else {
+                admit_tile<R>(L, S, e, pos, clock0 + pos, it);
+                ndecided = pos + 1;
+                if (SLOWMODE == 2) {
+                    cc_issue(L, sr, e, ccv, ccsize);
+                    ccfill = true;
+                }
+            }
+        }
+        if (nstream != 0x7fffffff && B >= nstream * sb + 14) break;
         // ---- prefetch: u of vb+2 (-> n next step); slowness and halos of vb+1
-        const BInfo b1 = brick_info<R, RZ>(L, p1, lx, ly, lxs, lys, rx, ry, bc);
+        const BInfo b1 = brick_info<R, RZ>(L, S, p1, nstream, lx, ly, lxs, lys, rx, ry, bc);
         {
             Pos p2 = p1;
-            pos_adv(p2, L);
-            const bool v2 = p2.vb >= 0 && p2.k < L.ntiles && p2.zbs < L.nzb;
+            pos_adv(p2, sb);
             uint32_t seg2 = OOB;
-            if (v2) {
-                int tx = rx ? L.ntx - 1 - p2.txs : p2.txs, ty = ry ? L.nty - 1 - p2.tys : p2.tys;
-                int zb = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
+            if (pos_valid(p2, nstream, L.nzb)) {
+                const int e2 = S.ring[p2.sp & 3];
+                const int tx = e2 & 0xfff, ty = (e2 >> 12) & 0xfff;
+                const int zb = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
                 seg2 = ((uint32_t)(ty * L.ntx + tx) * ((uint32_t)L.nzb * 512u) + (uint32_t)zb * 512u +
                         (uint32_t)(ly * 8 + lx) * 8u) * (uint32_t)sizeof(R);
             }
             bload8(ur, seg2, q);
         }
-        bool ccfill = false;
-        if (SLOWMODE == 2) {
-            ccfill = ccph == 0;                  // B + 1 == cckf * sb: lane (0,0) enters tile cckf next step
-            if (ccfill) cc_issue(L, sr, cckf, rx, ry, ccv, ccsize);
-        } else {
-            prefetch_slow<R, SLOWMODE>(L, sr, b1, fq);
-        }
+        if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, sr, b1, fq);
         bload8(ur, b1.hx, hxq);
         bload8(ur, b1.hy, hyq);
 
         // ---- the 8 z-slots of the current brick
         const int fl = b0.flags;
         const bool act = (fl & F_ACT) != 0;
-        bool changed = false;
+        bool changed = false, small = false;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int pj = RZ ? 7 - j : j;
@@ -488,13 +615,15 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
             const R ym = shfl_up8(r[pj]), ypv = shfl_down8(n[pj]);
             R fv;
             if (SLOWMODE == 2)
-                fv = (R)cc[b0.ccb + (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20)] * hr;
+                fv = (R)S.cc[b0.ccb + (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20)] * hr;
             else
-                fv = sf[pj * 64 + lane];
-            const R hxv = shx[pj * 8 + lys];
-            const R hyv = shy[(pj * 2 + hysel) * 8 + lxs];
-            const R xhv = xh[zabs * 8 + lys];
-            const R xup = !(fl & F_XP) ? self : (lxs > 0 ? xm : xhv);
+                fv = S.sf[pj * 64 + lane];
+            R hxv = S.shx[(pj * 2 + hxsel) * 8 + lys];
+            R hyv = S.shy[(pj * 2 + hysel) * 8 + lxs];
+            // keep the LDS reads unconditional (hipcc otherwise sinks them into
+            // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
+            asm volatile("" : "+v"(hxv), "+v"(hyv));
+            const R xup = !(fl & F_XP) ? self : (lxs > 0 ? xm : hxv);
             const R xdn = !(fl & F_XN) ? self : (lxs < 7 ? xpv : hxv);
             const R yup = !(fl & F_YP) ? self : (lys > 0 ? ym : hyv);
             const R ydn = !(fl & F_YN) ? self : (lys < 7 ? ypv : hyv);
@@ -509,66 +638,95 @@ __device__ __forceinline__ void sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsr
             const R ub = godunov_bl<FAST>(ux, uy, uz, fv, e);
             const bool upd = act && zabs < L.nz && !((fl >> (8 + pj)) & 1);
             const R nv = upd ? (self < ub ? self : ub) : self;
-            if (upd && nv < self && self >= T) notconv = true;
-            if (last_sweep && act && b0.x == 0 && b0.y == 0 && zabs == 0) ierr_last = upd ? e : 0;
-            changed |= nv != self;
+            const bool dec = nv < self;
+            if (dec && self >= T) notconv = true;
+            small |= dec && self < T;
+            if (act && b0.x == 0 && b0.y == 0 && zabs == 0) ierr_last = upd ? e : 0;
+            changed |= dec;
             r[pj] = nv;
-            // x-upwind halo of the next tile (lanes lx=7); other lanes write a private trash word
-            R *dst = (lxs == 7 && (fl & F_VALID)) ? xh + zabs * 8 + lys : trash + lane;
-            *dst = nv;
         }
 
-        // ---- write-back and convergence bookkeeping of the current brick
+        // ---- write-back, u0 at a tile's first visit of the iteration, change stamps
         bstore8(ur, changed ? b0.seg : OOB, r);
-        if (first_sweep) {
+        {
             bool need = false;
 #pragma unroll
             for (int i = 0; i < 8; i++) need |= c[i] < T;
-            bstore8(u0r, need ? b0.seg : OOB, c);
+            bstore8(u0r, (need && (fl & F_U0)) ? b0.seg : OOB, c);
         }
-        if (last_sweep) {
-            bool need = false;
-            if (act && !notconv) {
+        {
+            // lanes sit on at most 3 stream positions: lane (0,0)'s and the two before
+            const int sp0 = __builtin_amdgcn_readfirstlane(b0.sp);
+            const bool val = (fl & F_VALID) != 0;
 #pragma unroll
-                for (int i = 0; i < 8; i++) need |= (r[i] < T) && (b0.zb8 + i < L.nz);
-            }
-            if (__any(need)) {
-                R v0[8];
-                bload8(u0r, need ? b0.seg : OOB, v0);
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    R dl = v0[i] - r[i];
-                    dl = dl < (R)0 ? -dl : dl;
-                    if (need && b0.zb8 + i < L.nz && !(dl < tolr)) notconv = true;
+            for (int back = 0; back < 3; back++) {
+                const int pos = sp0 - back;
+                const bool mine = val && b0.sp == pos;
+                const bool ac = __any(changed && mine), as = __any(small && mine);
+                if ((ac || as) && lane == 0) {
+                    const int id = ring_tile(L, S.ring, pos);
+                    if (ac) S.lastchg[id] = clock0 + pos;
+                    if (as) S.smallit[id] = (unsigned short)(it + 1);
                 }
             }
         }
         asm volatile("" ::: "memory");
         // ---- stage the prefetched slowness/halos of vb+1 for the next step
         if (SLOWMODE == 2) {
-            if (ccfill) {
-                cc_write(cc, cck3, ccv, ccsize);
-                cckf++;
-                if (++cck3 == 3) cck3 = 0;
-            }
-            if (++ccph == L.sb) ccph = 0;
+            if (ccfill) cc_write(S.cc, (ndecided - 1) % 3, ccv, ccsize);
         } else {
 #pragma unroll
-            for (int i = 0; i < 8; i++) sf[i * 64 + lane] = fq[i] * hr;
+            for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
         }
-        if (lxs == 7) {
+        if (lxs == 0 || lxs == 7) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) shx[i * 8 + lys] = hxq[i];
+            for (int i = 0; i < 8; i++) S.shx[(i * 2 + hxsel) * 8 + lys] = hxq[i];
         }
         if (lys == 0 || lys == 7) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
+            for (int i = 0; i < 8; i++) S.shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
         }
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; }
         b0 = b1;
-        pos_adv(p1, L);
+        pos_adv(p1, sb);
+        if (++ph == sb) ph = 0;
+    }
+    visited += (unsigned long long)nstream;
+    return nstream;
+}
+
+// End-of-iteration check of the nodes below T: only tiles where such a node
+// changed in this iteration; u0 was stored at their first visit.
+template <typename R>
+__device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int it, bool &notconv)
+{
+    const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
+    const R T = (R)L.conv_thresh, tolr = (R)L.tol;
+    for (int base = 0; base < L.ntiles; base += 64) {
+        const int k = base + lane;
+        const bool flag = k < L.ntiles && S.smallit[k] == (unsigned short)(it + 1);
+        unsigned long long m = __ballot(flag);
+        while (m) {
+            const int id = base + __builtin_ctzll(m);
+            m &= m - 1;
+            const int tx = id % L.ntx, ty = id / L.ntx;
+            const int x = tx * 8 + lx, y = ty * 8 + ly;
+            for (int zb = 0; zb < L.nzb; zb++) {
+                const uint32_t seg = ((uint32_t)id * ((uint32_t)L.nzb * 512u) + (uint32_t)zb * 512u +
+                                      (uint32_t)lane * 8u) * (uint32_t)sizeof(R);
+                R u[8], v0[8];
+                bload8(ur, seg, u);
+                bload8(u0r, seg, v0);
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    R dl = v0[i] - u[i];
+                    dl = dl < (R)0 ? -dl : dl;
+                    if (x < L.nx && y < L.ny && zb * 8 + i < L.nz && u[i] < T && !(dl < tolr)) notconv = true;
+                }
+            }
+        }
     }
 }
 
@@ -658,19 +816,29 @@ __device__ __forceinline__ int next_solve(const FsmLaunch &L, int &pass)
     return -1;
 }
 
+// Diagonal order of the tiles for the (+x, +y) sweep: by txs + tys, then tys.
+// Other directions flip tx / ty; every tile comes after its upwind neighbours.
+__device__ void build_order(const FsmLaunch &L, int *order)
+{
+    for (int id = threadIdx.x; id < L.ntiles; id += 64) {
+        const int txs = id % L.ntx, tys = id / L.ntx, dg = txs + tys;
+        int rank = 0;
+        for (int e = 0; e < dg; e++)
+            rank += min(e, L.nty - 1) - max(0, e - L.ntx + 1) + 1;
+        rank += tys - max(0, dg - L.ntx + 1);
+        order[rank] = txs | (tys << 16);
+    }
+}
+
 template <typename R, int SLOWMODE, bool FAST>
 __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int *bcbox = reinterpret_cast<int *>(smem);                 // 192 B, 16-B multiple
-    float *cc = reinterpret_cast<float *>(smem + BC_LDS_BYTES); // [3][CC_MAX] cell cache (SLOWMODE 2)
-    R *xh = reinterpret_cast<R *>(smem + BC_LDS_BYTES + (SLOWMODE == 2 ? 3 * CC_MAX * 4 : 0));   // [nzb*8][8]
-    R *sf = xh + (size_t)L.nzb * 64;                            // [8][64] staged f = s*h
-    R *shx = sf + (SLOWMODE == 2 ? 0 : 512);                    // [8][8]   x-downwind halo
-    R *shy = shx + 64;                                          // [8][2][8] y halos
-    R *trash = shy + 128;                                       // [64]
+    const Smem<R> S = smem_bind<R>(L, smem);
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
+    build_order(L, S.order);
+    unsigned long long visited = 0;
     int pass = 0;
     for (;;) {
         const int snext = next_solve(L, pass);
@@ -691,33 +859,37 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
             slow_bytes = (uint32_t)(ncell * 4);
         }
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
+        for (int t = lane; t < L.ntiles; t += 64) {
+            S.lastproc[t] = -1; S.lastchg[t] = -1;       // every tile dirty for the first sweep
+            S.u0ep[t] = 0; S.smallit[t] = 0;
+        }
         BcBoxes bc;
-        bc.box = bcbox;
+        bc.box = S.box;
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
-        int iters = 0, ierr_last = 0;
+        int iters = 0, ierr_last = 0, clock = 0;
         if (ok) {
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
-                    const bool first = sw == 0, last = sw == 7;
                     if (sw & 4)
-                        sweep<R, SLOWMODE, FAST, true>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, cc, rx, ry,
-                                                       first, last, notconv, ierr_last);
+                        clock += sweep<R, SLOWMODE, FAST, true>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
+                                                                notconv, ierr_last, visited);
                     else
-                        sweep<R, SLOWMODE, FAST, false>(L, ur, u0r, sr, bc, xh, sf, shx, shy, trash, cc, rx, ry,
-                                                        first, last, notconv, ierr_last);
+                        clock += sweep<R, SLOWMODE, FAST, false>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
+                                                                 notconv, ierr_last, visited);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
                 iters = it + 1;
                 if (sweeps_left > 0 || L.max_sweeps < 0) {
+                    if (!__any(notconv)) verify_small<R>(L, ur, u0r, S, it, notconv);
                     if (!__any(notconv)) break;
                 }
             }
         }
-        // ierr: set only by the lane that owns node (0,0,0) in the last sweep
+        // ierr: from the last evaluation of node (0,0,0) (the reference's last update)
         int ierr = ierr_last;
         for (int o = 32; o > 0; o >>= 1) ierr = max(ierr, __shfl_xor(ierr, o, 64));
         if (!ok) ierr = 1;
@@ -737,6 +909,7 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
+    if (lane == 0 && L.tile_total && visited) atomicAdd(L.tile_total, visited);
 }
 
 // ---- layout conversion (x-fastest <-> brick), drop-in entry points only ----
