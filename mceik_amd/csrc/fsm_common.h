@@ -45,9 +45,11 @@ static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 // LDS of one solve wave (byte offsets, shared by host and device):
 //  0 BC boxes [MAX_SRC][6] int | 1 cell cache [3][256] float (cached mode) |
 //  2 diagonal tile order int | 3 lastproc int | 4 lastchg int | 5 u0 epoch u16 |
-//  6 small-change epoch u16 (all [ntiles]) | 7 stream ring [4] int |
-//  8 staged f [8][64] R (uncached) | 9 x halos [8][2][8] R | 10 y halos [8][2][8] R
+//  (all [ntiles]) 6 unused | 7 stream ring [4] int |
+//  8 staged f [8][64] R (uncached) | 9 x halos [8][2][8] R | 10 y halos [8][2][8] R |
+//  11 column info [4][64] uint4
 #define MCEIK_CC_MAX 256
+#define MCEIK_SMEM_ARRAYS 12
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
 static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, size_t es, size_t *off)
 {
@@ -60,16 +62,17 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[3] = o; o += mceik_align16(nt * 4);
     off[4] = o; o += mceik_align16(nt * 4);
     off[5] = o; o += mceik_align16(nt * 2);
-    off[6] = o; o += mceik_align16(nt * 2);
+    off[6] = o;                                   // (unused)
     off[7] = o; o += 16;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 128 * es;
     off[10] = o; o += 128 * es;
+    off[11] = o; o += 4 * 64 * 16;
     return o;
 }
 static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
 {
-    size_t off[11];
+    size_t off[MCEIK_SMEM_ARRAYS];
     return fsm_smem_layout(L, es, off);
 }
 #define MCEIK_MAX_LDS (64 * 1024)   // dynamic LDS without a launch attribute

@@ -150,11 +150,11 @@ __device__ __forceinline__ float bload1f(Rsrc r, uint32_t off)
 // y neighbours by ds_bpermute (lane -+ 8).  Tile-edge lanes get halo values.
 __device__ __forceinline__ float dpp_from_prev(float v)
 {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float dpp_from_next(float v)
 {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x101, 0xf, 0xf, true));
 }
 __device__ __forceinline__ double dpp_from_prev(double v)
 {
@@ -170,10 +170,19 @@ __device__ __forceinline__ double dpp_from_next(double v)
     unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x101, 0xf, 0xf, false);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-template <typename R>
-__device__ __forceinline__ R shfl_up8(R v) { return __shfl_up(v, 8, 64); }
-template <typename R>
-__device__ __forceinline__ R shfl_down8(R v) { return __shfl_down(v, 8, 64); }
+// y neighbours: ds_bpermute from lane -/+ 8 (byte addresses precomputed once;
+// lanes 0..7 / 56..63 receive a wrapped value and use the y halo instead)
+__device__ __forceinline__ float bperm(int addr, float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double bperm(int addr, double v)
+{
+    unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    unsigned lo = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)u);
+    unsigned hi = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(u >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 
 // Correctly rounded sqrt for normal positive x (LLVM's expansion without the
 // denormal rescale and zero/inf fix-up).  Used only where the radicand that
@@ -247,8 +256,8 @@ struct Smem {
     int *order;                  // diagonal order: txs | tys << 16   [ntiles]
     int *lastproc, *lastchg;     // stream clock of the last visit / last visit with a change
     unsigned short *u0ep;        // iteration+1 of the last u0 store of the tile
-    unsigned short *smallit;     // iteration+1 of the last change of a node below T
     int *ring;                   // stream entries of positions p & 3: tx | ty << 12 | u0 flag << 24
+    u4v *cinfo;                  // [4][64] column info of every lane for positions p & 3
     R *sf, *shx, *shy;           // staged slowness*h (modes 0,1) and halos
 };
 
@@ -257,7 +266,7 @@ struct Smem {
 template <typename R>
 __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *base)
 {
-    size_t off[11];
+    size_t off[MCEIK_SMEM_ARRAYS];
     fsm_smem_layout(L, sizeof(R), off);
     Smem<R> S;
     S.box = reinterpret_cast<int *>(base + off[0]);
@@ -266,43 +275,53 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     S.lastproc = reinterpret_cast<int *>(base + off[3]);
     S.lastchg = reinterpret_cast<int *>(base + off[4]);
     S.u0ep = reinterpret_cast<unsigned short *>(base + off[5]);
-    S.smallit = reinterpret_cast<unsigned short *>(base + off[6]);
     S.ring = reinterpret_cast<int *>(base + off[7]);
     S.sf = reinterpret_cast<R *>(base + off[8]);
     S.shx = reinterpret_cast<R *>(base + off[9]);
     S.shy = reinterpret_cast<R *>(base + off[10]);
+    S.cinfo = reinterpret_cast<u4v *>(base + off[11]);
     return S;
 }
 
 // Position of a lane in the stream of one sweep: stream position sp (tile
 // ordinal within the sweep) and z-brick zbs, advanced one virtual brick per
-// macro step.  sp3 = sp mod 3 selects the cell-cache buffer.
+// macro step.
 struct Pos {
-    int vb, sp, zbs, sp3;
+    int vb, sp, zbs;
 };
 __device__ __forceinline__ void pos_init(Pos &p, int vb, int sb)
 {
     p.vb = vb;
     const int v = vb < 0 ? 0 : vb;
-    p.sp = v / sb; p.zbs = v - p.sp * sb; p.sp3 = p.sp % 3;
+    p.sp = v / sb; p.zbs = v - p.sp * sb;
 }
 __device__ __forceinline__ void pos_adv(Pos &p, int sb)
 {
     if (p.vb >= 0 && ++p.zbs == sb) {
         p.zbs = 0; p.sp++;
-        if (++p.sp3 == 3) p.sp3 = 0;
     }
     p.vb++;
 }
+__device__ __forceinline__ bool pos_valid(const Pos &p, int nstream, int nzb)
+{
+    return p.vb >= 0 && p.sp < nstream && p.zbs < nzb;
+}
 
-enum { F_VALID = 1, F_ACT = 2, F_XP = 4, F_XN = 8, F_YP = 16, F_YN = 32, F_U0 = 64 };
+// Column flags (written at admission, per lane and position) and brick flags.
+enum {
+    C_ACT = 1,      // column inside the grid
+    C_U0 = 2,       // first visit of the tile in this iteration: store u0
+    C_PART = 4,     // tile cut by the grid's x or y end (generic path)
+    C_00 = 8,       // column of node (0,0,0) (ierr, generic path)
+    C_BC = 16,      // column crosses a boundary-condition box in x and y
+    F_VALID = 32, F_FIRST = 64, F_LAST = 128, F_SLOW = 256
+};
 
 // What a lane needs about one of its bricks.
 struct BInfo {
     uint32_t seg, hx, hy;    // byte offsets (u buffer): own segment, x halo, y halo (OOB if none)
-    int zb8, flags, x, y;    // bits 8..15 of flags: BC z-slots (physical) of this column segment
-    int ccb;                 // cell-cache LDS index of this column's cell column (SLOWMODE 2)
-    int sp;                  // stream position (sweep-local) of the brick's tile
+    int zb8, fl, ccb, sp;    // fl: C_* | F_*; ccb: cell-cache index of the brick (SLOWMODE 2)
+    int bcm;                 // BC z-slots of the segment (generic path)
 };
 
 // Cell range of a tile along one axis: first cell and count.
@@ -313,67 +332,91 @@ __device__ __forceinline__ void tile_cells(int t, int n, unsigned magic, int &c0
     nc = (int)(((unsigned)b * magic) >> 20) - c0 + 1;
 }
 
-__device__ __forceinline__ bool pos_valid(const Pos &p, int nstream, int nzb)
+// Column info of this lane for tile `entry` at stream position pos.  The x/y
+// halo of a tile-edge lane is the neighbour column, or the lane's own column
+// where the grid ends (the reference's missing neighbour is the node itself:
+// the halo then holds exactly the node's old value); interior lanes: OOB.
+template <typename R>
+__device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc, int entry, int pos, int u0flag,
+                                           int lx, int ly, int lxs, int lys, int rx, int ry)
 {
-    return p.vb >= 0 && p.sp < nstream && p.zbs < nzb;
-}
-
-template <typename R, bool RZ>
-__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
-                                            int lx, int ly, int lxs, int lys, int rx, int ry, const BcBoxes &bc)
-{
-    BInfo b;
-    const bool valid = pos_valid(p, nstream, L.nzb);
-    const int e = valid ? S.ring[p.sp & 3] : 0;
-    const int tx = e & 0xfff, ty = (e >> 12) & 0xfff;
-    const int zb = valid ? (RZ ? L.nzb - 1 - p.zbs : p.zbs) : 0;
-    b.sp = p.sp;
-    b.zb8 = zb * 8;
-    b.x = tx * 8 + lx; b.y = ty * 8 + ly;
-    const bool inxy = b.x < L.nx && b.y < L.ny;
-    const bool xlo = b.x > 0, xhi = b.x < L.nx - 1, ylo = b.y > 0, yhi = b.y < L.ny - 1;
-    const bool xp = rx ? xhi : xlo, xn = rx ? xlo : xhi, yp = ry ? yhi : ylo, yn = ry ? ylo : yhi;
-    int fl = (valid ? F_VALID : 0) | ((valid && inxy) ? F_ACT : 0) | (xp ? F_XP : 0) | (xn ? F_XN : 0) |
-             (yp ? F_YP : 0) | (yn ? F_YN : 0) | ((valid && ((e >> 24) & 1)) ? F_U0 : 0);
-    const uint32_t es = sizeof(R);
-    const uint32_t stride_tile = (uint32_t)L.nzb * 512u;
-    b.seg = valid ? ((uint32_t)(ty * L.ntx + tx) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lx) * 8u) * es : OOB;
-    // x halo: lane lx'=0 takes the sweep-upwind column (new values, from HBM),
-    // lane lx'=7 the sweep-downwind column of the next tile (old values)
-    b.hx = OOB;
-    if (valid && ((lxs == 0 && xp) || (lxs == 7 && xn))) {
-        const bool up = lxs == 0;
-        const int txh = (up != (rx != 0)) ? tx - 1 : tx + 1;
-        const int lxh = (up != (rx != 0)) ? 7 : 0;
-        b.hx = ((uint32_t)(ty * L.ntx + txh) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(ly * 8 + lxh) * 8u) * es;
+    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
+    const int x = tx * 8 + lx, y = ty * 8 + ly;
+    const uint32_t es = sizeof(R), st = (uint32_t)L.nzb * 512u;
+    const uint32_t col = ((uint32_t)(ty * L.ntx + tx) * st + (uint32_t)(ly * 8 + lx) * 8u) * es;
+    uint32_t hx = OOB, hy = OOB;
+    if (lxs == 0 || lxs == 7) {
+        const int xn = x + (((lxs == 0) != (rx != 0)) ? -1 : 1);
+        hx = (xn >= 0 && xn < L.nx) ? ((uint32_t)(ty * L.ntx + (xn >> 3)) * st + (uint32_t)(ly * 8 + (xn & 7)) * 8u) * es
+                                     : col;
     }
-    b.hy = OOB;
-    if (valid && ((lys == 0 && yp) || (lys == 7 && yn))) {
-        const bool up = lys == 0;
-        const int tyh = (up != (ry != 0)) ? ty - 1 : ty + 1;
-        const int lyh = (up != (ry != 0)) ? 7 : 0;
-        b.hy = ((uint32_t)(tyh * L.ntx + tx) * stride_tile + (uint32_t)zb * 512u + (uint32_t)(lyh * 8 + lx) * 8u) * es;
+    if (lys == 0 || lys == 7) {
+        const int yn = y + (((lys == 0) != (ry != 0)) ? -1 : 1);
+        hy = (yn >= 0 && yn < L.ny) ? ((uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)((yn & 7) * 8 + lx) * 8u) * es
+                                     : col;
     }
-    // BC z-slots of this column segment
-    unsigned m = 0;
+    int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
+    if (u0flag) m |= C_U0;
+    if (tx * 8 + 8 > L.nx || ty * 8 + 8 > L.ny) m |= C_PART;
+    if (x == 0 && y == 0) m |= C_00;
     for (int k = 0; k < bc.n; k++) {
         const int *q = bc.box + 6 * k;
-        if (b.x >= q[0] && b.x <= q[1] && b.y >= q[2] && b.y <= q[3]) {
-            int lo = q[4] - b.zb8, hi = q[5] - b.zb8;
-            lo = lo < 0 ? 0 : lo; hi = hi > 7 ? 7 : hi;
-            if (lo <= hi) m |= ((2u << hi) - (1u << lo));
+        if (x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]) m |= C_BC;
+    }
+    int cx0, ncxt, cy0, ncyt;
+    tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
+    tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
+    const int xc = x < L.nx ? x : L.nx - 1, yc = y < L.ny ? y : L.ny - 1;
+    const int cxl = (int)(((unsigned)xc * L.magic_rx) >> 20) - cx0;
+    const int cyl = (int)(((unsigned)yc * L.magic_ry) >> 20) - cy0;
+    const int ccb = (pos % 3) * CC_MAX + (cyl * ncxt + cxl) * L.ncz;
+    u4v v;
+    v.x = col; v.y = hx; v.z = hy; v.w = (unsigned)(m | (ccb << 8));
+    return v;
+}
+
+template <typename R, bool RZ, int ZSH>
+__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
+                                            int lx, int ly, const BcBoxes &bc)
+{
+    BInfo b;
+    const int lane = threadIdx.x;
+    const bool valid = pos_valid(p, nstream, L.nzb);
+    const u4v ci = S.cinfo[(p.sp & 3) * 64 + lane];
+    const int zb = valid ? (RZ ? L.nzb - 1 - p.zbs : p.zbs) : 0;
+    const uint32_t zoff = (uint32_t)zb * 512u * (uint32_t)sizeof(R);
+    b.seg = valid ? ci.x + zoff : OOB;
+    b.hx = valid ? ci.y + zoff : OOB;
+    b.hy = valid ? ci.z + zoff : OOB;
+    b.zb8 = zb * 8;
+    b.sp = p.sp;
+    const int meta = (int)ci.w;
+    int fl = valid ? ((meta & 0xff) | F_VALID) : 0;
+    if (zb == (RZ ? L.nzb - 1 : 0)) fl |= F_FIRST;
+    if (zb == (RZ ? 0 : L.nzb - 1)) fl |= F_LAST;
+    bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && b.zb8 + 8 > L.nz);
+    b.bcm = 0;
+    if (__any(fl & C_BC)) {
+        // BC z-slots of this column segment (rare: columns through a source box)
+        const int e = S.ring[p.sp & 3];
+        const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
+        unsigned m = 0;
+        if (fl & C_BC) {
+            for (int k = 0; k < bc.n; k++) {
+                const int *q = bc.box + 6 * k;
+                if (x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]) {
+                    int lo = q[4] - b.zb8, hi = q[5] - b.zb8;
+                    lo = lo < 0 ? 0 : lo; hi = hi > 7 ? 7 : hi;
+                    if (lo <= hi) m |= ((2u << hi) - (1u << lo));
+                }
+            }
         }
+        b.bcm = (int)m;
+        slow |= m != 0;
     }
-    b.flags = fl | (int)(m << 8);
-    {
-        int cx0, ncxt, cy0, ncyt;
-        tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
-        tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
-        const int x = b.x < L.nx ? b.x : L.nx - 1, y = b.y < L.ny ? b.y : L.ny - 1;
-        const int cxl = (int)(((unsigned)x * L.magic_rx) >> 20) - cx0;
-        const int cyl = (int)(((unsigned)y * L.magic_ry) >> 20) - cy0;
-        b.ccb = valid ? p.sp3 * CC_MAX + (cyl * ncxt + cxl) * L.ncz : 0;
-    }
+    if (slow) fl |= F_SLOW;
+    b.fl = fl;
+    b.ccb = (meta >> 8) + (ZSH >= 0 ? (b.zb8 >> (ZSH < 0 ? 0 : ZSH)) : 0);
     return b;
 }
 
@@ -387,17 +430,21 @@ __device__ __forceinline__ double slow_at(const FsmLaunch &L, const void *slow_m
 }
 
 // Slowness of the 8 nodes of a segment (prefetch; multiplied by h when staged).
+// Modes 0 and 1 only; the column's x, y come from the stream ring.
 template <typename R, int SLOWMODE>
-__device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, Rsrc sr, const BInfo &b, R (&s)[8])
+__device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R> &S, Rsrc sr, const BInfo &b,
+                                              int lx, int ly, R (&s)[8])
 {
     if (SLOWMODE == 0) {
-        bload8(sr, (b.flags & F_VALID) ? b.seg : OOB, s);
+        bload8(sr, b.seg, s);
     } else {
+        const int e = S.ring[b.sp & 3];
         const uint32_t mx = L.magic_rx, my = L.magic_ry, mz = L.magic_rz;
-        const int x = b.x < L.nx ? b.x : L.nx - 1, y = b.y < L.ny ? b.y : L.ny - 1;
+        int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
+        x = x < L.nx ? x : L.nx - 1; y = y < L.ny ? y : L.ny - 1;
         const uint32_t col = ((uint32_t)y * my >> 20) * (uint32_t)L.ncx + ((uint32_t)x * mx >> 20);
         const uint32_t plane = (uint32_t)L.ncx * L.ncy;
-        const bool v = (b.flags & F_VALID) != 0;
+        const bool v = (b.fl & F_VALID) != 0;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             int z = b.zb8 + i;
@@ -410,9 +457,10 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, Rsrc sr, const
 
 // Cell cache (SLOWMODE 2): the slowness cells a tile touches (2 x 2 x ncz at
 // nref = 4), three buffers indexed by stream position mod 3.  Loads for the
-// tile at position k are issued one macro step before lane (0,0) enters it and
-// written at the end of that step; the buffer they replace (position k-3) has
-// no reader left (sb >= 11).
+// tile at position k are issued two macro steps before lane (0,0) enters it
+// and written at the end of that step; the buffer they replace (position k-3)
+// has no reader left (sb >= 11).  fp32 entries hold f = s*h (the product the
+// update uses, rounded once as before); fp64 entries hold s.
 __device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int entry, float (&v)[CC_MAX / 64], int &size)
 {
     const int lane = threadIdx.x;
@@ -430,13 +478,14 @@ __device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int entry,
         v[r] = bload1f(sr, idx < size ? off : OOB);
     }
 }
-__device__ __forceinline__ void cc_write(float *cc, int buf, const float (&v)[CC_MAX / 64], int size)
+template <typename R>
+__device__ __forceinline__ void cc_write(float *cc, int buf, const float (&v)[CC_MAX / 64], int size, float h)
 {
     const int lane = threadIdx.x;
 #pragma unroll
     for (int r = 0; r < CC_MAX / 64; r++) {
         const int idx = lane + 64 * r;
-        if (idx < size) cc[buf * CC_MAX + idx] = v[r];
+        if (idx < size) cc[buf * CC_MAX + idx] = sizeof(R) == 4 ? v[r] * h : v[r];
     }
 }
 
@@ -480,13 +529,17 @@ __device__ int choose_tile(const FsmLaunch &L, const Smem<R> &S, int &cursor, in
     return -1;
 }
 
-// Admit the chosen tile at stream position pos (all lanes call; lane 0 writes).
+// Admit the chosen tile at stream position pos: every lane writes its column
+// info, lane 0 the ring entry and the tile's clocks.
 template <typename R>
-__device__ __forceinline__ void admit_tile(const FsmLaunch &L, const Smem<R> &S, int entry, int pos, int clock, int it)
+__device__ __forceinline__ void admit_tile(const FsmLaunch &L, const Smem<R> &S, const BcBoxes &bc, int entry, int pos,
+                                           int clock, int it, int lx, int ly, int lxs, int lys, int rx, int ry)
 {
     const int id = (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
     const int u0flag = S.u0ep[id] != (unsigned short)(it + 1);
+    const u4v ci = column_info<R>(L, bc, entry, pos, u0flag, lx, ly, lxs, lys, rx, ry);
     asm volatile("" ::: "memory");
+    S.cinfo[(pos & 3) * 64 + threadIdx.x] = ci;
     if (threadIdx.x == 0) {
         S.u0ep[id] = (unsigned short)(it + 1);
         S.lastproc[id] = clock;
@@ -502,10 +555,152 @@ __device__ __forceinline__ int ring_tile(const FsmLaunch &L, const int *ring, in
     return (e & 0xfff) + ((e >> 12) & 0xfff) * L.ntx;
 }
 
+// min of two travel times.  Values in the field are never NaN or -0 (every
+// update is clamped to FLT_MAX, sources are ts + d*s >= +0), so for fp32 the
+// unsigned order of the bit patterns is the float order: v_min_u32 needs no
+// IEEE canonicalisation of its inputs (v_min_f32 does).
+__device__ __forceinline__ float fmin_(float a, float b)
+{
+    const unsigned ia = __builtin_bit_cast(unsigned, a), ib = __builtin_bit_cast(unsigned, b);
+    return __builtin_bit_cast(float, __builtin_elementwise_min(ia, ib));
+}
+__device__ __forceinline__ double fmin_(double a, double b) { return __builtin_fmin(a, b); }
+
+// Godunov update without the error code (fast path): fp32 values identical to
+// godunov_bl (a1 == UN or an overflowing / NaN candidate gives UN either way).
+template <bool FAST>
+__device__ __forceinline__ float godunov_v(float a, float b, float c, float f)
+{
+    // sort by bit pattern (non-negative, non-NaN inputs; see fmin_)
+    const unsigned ia = __builtin_bit_cast(unsigned, a), ib = __builtin_bit_cast(unsigned, b),
+                   ic = __builtin_bit_cast(unsigned, c);
+    const unsigned lo = __builtin_elementwise_min(ia, ib), hi = __builtin_elementwise_max(ia, ib);
+    const float a1 = __builtin_bit_cast(float, __builtin_elementwise_min(lo, ic));
+    const float a3 = __builtin_bit_cast(float, __builtin_elementwise_max(hi, ic));
+    const float a2 = __builtin_bit_cast(float, __builtin_elementwise_max(lo, __builtin_elementwise_min(hi, ic)));
+    const float d2 = a2 - a1, d3 = a3 - a1;
+    const float r2 = (2.0f * f) * f - d2 * d2;
+    const float y2 = 0.5f * (d2 + (FAST ? sqrt_normal(r2) : __builtin_sqrtf(r2)));
+    const float sm = d2 + d3;
+    const float q = ((d2 * d2) + (d3 * d3)) - f * f;
+    const float disc = sm * sm - 3.0f * q;
+    const float y3 = (sm + (FAST ? sqrt_normal(disc) : __builtin_sqrtf(disc))) * (1.0f / 3.0f);
+    const float y = !(f > d2) ? f : (!(y2 > d3) ? y2 : y3);
+    // x >= UN, +inf or NaN -> UN: unsigned min with the bits of FLT_MAX (x >= +0)
+    const unsigned ix = __builtin_bit_cast(unsigned, a1 + y);
+    return __builtin_bit_cast(float, __builtin_elementwise_min(ix, 0x7f7fffffu));
+}
+template <bool FAST>
+__device__ __forceinline__ double godunov_v(double a, double b, double c, double f)
+{
+    int e;
+    return godunov(a, b, c, f, e);
+}
+
+// The 8 z-slots of the current brick.  GENERIC: any brick (grid-edge columns
+// of cut tiles, cut z-bricks, BC nodes, node (0,0,0) with the reference's
+// ierr); otherwise the brick is interior to the grid in x, y and z up to the
+// sweep-order first/last brick, no lane holds a BC node, and every lane's
+// missing x/y neighbours are already its own old values (column_info).
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC>
+__device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, R (&c)[8],
+                                             R (&n)[8], R (&r)[8], int lx, int ly, int rx, int ry,
+                                             bool &changed, bool &nc, int &ierr_last)
+{
+    const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3;
+    const int hxsel = lxs == 7, hysel = lys >= 4;
+    const R hr = (R)L.h, T = (R)L.conv_thresh;
+    const int fl = b0.fl;
+    bool xp = true, xn = true, yp = true, yn = true, act = true;
+    if (GENERIC) {
+        const int e = S.ring[b0.sp & 3];
+        const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
+        const bool xlo = x > 0, xhi = x < L.nx - 1, ylo = y > 0, yhi = y < L.ny - 1;
+        xp = rx ? xhi : xlo; xn = rx ? xlo : xhi; yp = ry ? yhi : ylo; yn = ry ? ylo : yhi;
+        act = (fl & C_ACT) != 0;
+    }
+    const bool first = (fl & F_FIRST) != 0, last = (fl & F_LAST) != 0;
+    int aup = ((lane - 8) & 63) * 4, adn = ((lane + 8) & 63) * 4;
+    asm volatile("" : "+v"(aup), "+v"(adn));
+    // x and y neighbours of all 8 slots first: they come from the other lanes'
+    // r (updated in their previous step) and n, which this step does not
+    // modify, so the 16 lane exchanges and the LDS reads overlap.
+    R ux[8], uy[8], fvs[8];
+#pragma unroll
+    for (int pj = 0; pj < 8; pj++) {
+        const R self = c[pj];
+        const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
+        const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
+        R fv;
+        if (SLOWMODE == 2) {
+            if (ZSH >= 0 && !GENERIC) {
+                fv = (R)S.cc[b0.ccb + (pj >> (ZSH < 0 ? 0 : ZSH))];
+            } else {
+                const int zabs = b0.zb8 + pj;
+                fv = (R)S.cc[b0.ccb + (ZSH >= 0 ? (pj >> (ZSH < 0 ? 0 : ZSH))
+                                                : (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20))];
+            }
+            if (sizeof(R) == 8) fv *= hr;         // fp32 entries already hold s*h
+        } else {
+            fv = S.sf[pj * 64 + lane];
+        }
+        R hxv = S.shx[(pj * 2 + hxsel) * 8 + lys];
+        R hyv = S.shy[(pj * 2 + hysel) * 8 + lxs];
+        // keep the LDS reads unconditional (hipcc otherwise sinks them into
+        // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
+        asm volatile("" : "+v"(hxv), "+v"(hyv));
+        R xup = lxs > 0 ? xm : hxv;
+        R xdn = lxs < 7 ? xpv : hxv;
+        R yup = lys > 0 ? ym : hyv;
+        R ydn = lys < 7 ? ypv : hyv;
+        if (GENERIC) {
+            xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
+        }
+        ux[pj] = fmin_(xup, xdn);
+        uy[pj] = fmin_(yup, ydn);
+        fvs[pj] = fv;
+    }
+    // then the z chain in sweep order
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int pj = RZ ? 7 - j : j;
+        const int pprev = RZ ? pj + 1 : pj - 1;
+        const int pnext = RZ ? pj - 1 : pj + 1;
+        const R self = c[pj];
+        R zup, zdn;
+        if (GENERIC) {
+            const int zabs = b0.zb8 + pj;
+            const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
+            const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
+            zup = zp_ex ? (j > 0 ? r[pprev] : r[RZ ? 0 : 7]) : self;
+            zdn = zn_ex ? (j < 7 ? c[pnext] : n[RZ ? 7 : 0]) : self;
+        } else {
+            zup = j > 0 ? r[pprev] : (first ? self : r[RZ ? 0 : 7]);
+            zdn = j < 7 ? c[pnext] : (last ? self : n[RZ ? 7 : 0]);
+        }
+        const R uz = fmin_(zup, zdn);
+        R nv;
+        if (GENERIC) {
+            const int zabs = b0.zb8 + pj;
+            int e;
+            const R ub = godunov_bl<FAST>(ux[pj], uy[pj], uz, fvs[pj], e);
+            const bool upd = act && zabs < L.nz && !((b0.bcm >> pj) & 1);
+            nv = upd ? fmin_(self, ub) : self;
+            if ((fl & C_00) && zabs == 0) ierr_last = upd ? e : 0;
+        } else {
+            nv = fmin_(self, godunov_v<FAST>(ux[pj], uy[pj], uz, fvs[pj]));
+        }
+        const bool dec = nv < self;
+        nc |= dec && self >= T;
+        changed |= dec;
+        r[pj] = nv;
+    }
+}
+
 // One Gauss-Seidel sweep over the grid in direction (rx, ry, RZ): only the
 // tiles admitted by choose_tile are visited.  Returns the number of stream
 // positions used (the clock advance).
-template <typename R, int SLOWMODE, bool FAST, bool RZ>
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
                                      const Smem<R> &S, int rx, int ry, int it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned long long &visited)
@@ -522,7 +717,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     {
         const int e = choose_tile<R>(L, S, cursor, -1, -1, rx, ry);
         if (e < 0) return 0;                                // nothing changed near any tile: skip the sweep
-        admit_tile<R>(L, S, e, 0, clock0, it);
+        admit_tile<R>(L, S, bc, e, 0, clock0, it, lx, ly, lxs, lys, rx, ry);
         ndecided = 1;
     }
     R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8];
@@ -530,20 +725,20 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     int ccsize = 0;
     Pos p1;
     pos_init(p1, -d, sb);
-    BInfo b0 = brick_info<R, RZ>(L, S, p1, nstream, lx, ly, lxs, lys, rx, ry, bc);
+    BInfo b0 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
     // prologue: c = brick(vb0), n = brick(vb0+1); stage f and halos of vb0
     bload8(ur, b0.seg, c);
     if (SLOWMODE == 2) {
         cc_issue(L, sr, S.ring[0] & 0xffffff, ccv, ccsize);
-        cc_write(S.cc, 0, ccv, ccsize);
+        cc_write<R>(S.cc, 0, ccv, ccsize, (float)L.h);
     } else {
-        prefetch_slow<R, SLOWMODE>(L, sr, b0, fq);
+        prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
     }
     bload8(ur, b0.hx, hxq);
     bload8(ur, b0.hy, hyq);
     pos_adv(p1, sb);
     {
-        BInfo b1 = brick_info<R, RZ>(L, S, p1, nstream, lx, ly, lxs, lys, rx, ry, bc);
+        BInfo b1 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
         bload8(ur, b1.seg, n);
     }
 #pragma unroll
@@ -562,7 +757,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     asm volatile("" ::: "memory");
 
     int ph = 2 % sb;                 // (B + 2) mod sb: 0 when lane (0,0)'s vb+2 starts a new position
-    for (int B = 0; B < (nstream == 0x7fffffff ? 0x7fffffff : nstream * sb + 14); B++) {
+    for (int B = 0;; B++) {
         // ---- stream decision for the position lane (0,0) prefetches next
         bool ccfill = false;
         if (ph == 0 && nstream == 0x7fffffff) {
@@ -572,7 +767,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             if (e < 0) {
                 nstream = pos;
             } else {
-                admit_tile<R>(L, S, e, pos, clock0 + pos, it);
+                admit_tile<R>(L, S, bc, e, pos, clock0 + pos, it, lx, ly, lxs, lys, rx, ry);
                 ndecided = pos + 1;
                 if (SLOWMODE == 2) {
                     cc_issue(L, sr, e, ccv, ccsize);
@@ -582,98 +777,51 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
         if (nstream != 0x7fffffff && B >= nstream * sb + 14) break;
         // ---- prefetch: u of vb+2 (-> n next step); slowness and halos of vb+1
-        const BInfo b1 = brick_info<R, RZ>(L, S, p1, nstream, lx, ly, lxs, lys, rx, ry, bc);
+        const BInfo b1 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
         {
             Pos p2 = p1;
             pos_adv(p2, sb);
-            uint32_t seg2 = OOB;
-            if (pos_valid(p2, nstream, L.nzb)) {
-                const int e2 = S.ring[p2.sp & 3];
-                const int tx = e2 & 0xfff, ty = (e2 >> 12) & 0xfff;
-                const int zb = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
-                seg2 = ((uint32_t)(ty * L.ntx + tx) * ((uint32_t)L.nzb * 512u) + (uint32_t)zb * 512u +
-                        (uint32_t)(ly * 8 + lx) * 8u) * (uint32_t)sizeof(R);
-            }
-            bload8(ur, seg2, q);
+            const bool v2 = pos_valid(p2, nstream, L.nzb);
+            const uint32_t col2 = S.cinfo[(p2.sp & 3) * 64 + lane].x;
+            const int zb2 = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
+            bload8(ur, v2 ? col2 + (uint32_t)zb2 * 512u * (uint32_t)sizeof(R) : OOB, q);
         }
-        if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, sr, b1, fq);
+        if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
         bload8(ur, b1.hx, hxq);
         bload8(ur, b1.hy, hyq);
 
         // ---- the 8 z-slots of the current brick
-        const int fl = b0.flags;
-        const bool act = (fl & F_ACT) != 0;
-        bool changed = false, small = false;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int pj = RZ ? 7 - j : j;
-            const int pprev = RZ ? pj + 1 : pj - 1;
-            const int pnext = RZ ? pj - 1 : pj + 1;
-            const int zabs = b0.zb8 + pj;
-            const R self = c[pj];
-            const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
-            const R ym = shfl_up8(r[pj]), ypv = shfl_down8(n[pj]);
-            R fv;
-            if (SLOWMODE == 2)
-                fv = (R)S.cc[b0.ccb + (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20)] * hr;
-            else
-                fv = S.sf[pj * 64 + lane];
-            R hxv = S.shx[(pj * 2 + hxsel) * 8 + lys];
-            R hyv = S.shy[(pj * 2 + hysel) * 8 + lxs];
-            // keep the LDS reads unconditional (hipcc otherwise sinks them into
-            // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
-            asm volatile("" : "+v"(hxv), "+v"(hyv));
-            const R xup = !(fl & F_XP) ? self : (lxs > 0 ? xm : hxv);
-            const R xdn = !(fl & F_XN) ? self : (lxs < 7 ? xpv : hxv);
-            const R yup = !(fl & F_YP) ? self : (lys > 0 ? ym : hyv);
-            const R ydn = !(fl & F_YN) ? self : (lys < 7 ? ypv : hyv);
-            const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
-            const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
-            const R zup = zp_ex ? (j > 0 ? r[pprev] : r[RZ ? 0 : 7]) : self;
-            const R zdn = zn_ex ? (j < 7 ? c[pnext] : n[RZ ? 7 : 0]) : self;
-            const R ux = xup < xdn ? xup : xdn;
-            const R uy = yup < ydn ? yup : ydn;
-            const R uz = zup < zdn ? zup : zdn;
-            int e;
-            const R ub = godunov_bl<FAST>(ux, uy, uz, fv, e);
-            const bool upd = act && zabs < L.nz && !((fl >> (8 + pj)) & 1);
-            const R nv = upd ? (self < ub ? self : ub) : self;
-            const bool dec = nv < self;
-            if (dec && self >= T) notconv = true;
-            small |= dec && self < T;
-            if (act && b0.x == 0 && b0.y == 0 && zabs == 0) ierr_last = upd ? e : 0;
-            changed |= dec;
-            r[pj] = nv;
-        }
+        bool changed = false, nc = false;
+        if (__any(b0.fl & F_SLOW))
+            brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, lx, ly, rx, ry, changed, nc,
+                                                           ierr_last);
+        else
+            brick_update<R, SLOWMODE, FAST, RZ, ZSH, false>(L, S, b0, c, n, r, lx, ly, rx, ry, changed, nc,
+                                                            ierr_last);
+        const bool val = (b0.fl & F_VALID) != 0;
+        changed = changed && val;
+        notconv |= nc && val;
 
         // ---- write-back, u0 at a tile's first visit of the iteration, change stamps
         bstore8(ur, changed ? b0.seg : OOB, r);
         {
-            bool need = false;
-#pragma unroll
-            for (int i = 0; i < 8; i++) need |= c[i] < T;
-            bstore8(u0r, (need && (fl & F_U0)) ? b0.seg : OOB, c);
+            R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
+            bstore8(u0r, (m < T && (b0.fl & C_U0)) ? b0.seg : OOB, c);
         }
         {
             // lanes sit on at most 3 stream positions: lane (0,0)'s and the two before
             const int sp0 = __builtin_amdgcn_readfirstlane(b0.sp);
-            const bool val = (fl & F_VALID) != 0;
 #pragma unroll
             for (int back = 0; back < 3; back++) {
                 const int pos = sp0 - back;
                 const bool mine = val && b0.sp == pos;
-                const bool ac = __any(changed && mine), as = __any(small && mine);
-                if ((ac || as) && lane == 0) {
-                    const int id = ring_tile(L, S.ring, pos);
-                    if (ac) S.lastchg[id] = clock0 + pos;
-                    if (as) S.smallit[id] = (unsigned short)(it + 1);
-                }
+                if (__any(changed && mine) && lane == 0) S.lastchg[ring_tile(L, S.ring, pos)] = clock0 + pos;
             }
         }
         asm volatile("" ::: "memory");
         // ---- stage the prefetched slowness/halos of vb+1 for the next step
         if (SLOWMODE == 2) {
-            if (ccfill) cc_write(S.cc, (ndecided - 1) % 3, ccv, ccsize);
+            if (ccfill) cc_write<R>(S.cc, (ndecided - 1) % 3, ccv, ccsize, (float)L.h);
         } else {
 #pragma unroll
             for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
@@ -697,16 +845,17 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     return nstream;
 }
 
-// End-of-iteration check of the nodes below T: only tiles where such a node
-// changed in this iteration; u0 was stored at their first visit.
+// End-of-iteration check of the nodes below T (run only when no node >= T
+// changed): the tiles that changed in this iteration (lastchg >= the
+// iteration's first clock); u0 was stored at their first visit.
 template <typename R>
-__device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int it, bool &notconv)
+__device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int clock_it, bool &notconv)
 {
     const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
     const R T = (R)L.conv_thresh, tolr = (R)L.tol;
     for (int base = 0; base < L.ntiles; base += 64) {
         const int k = base + lane;
-        const bool flag = k < L.ntiles && S.smallit[k] == (unsigned short)(it + 1);
+        const bool flag = k < L.ntiles && S.lastchg[k] >= clock_it;
         unsigned long long m = __ballot(flag);
         while (m) {
             const int id = base + __builtin_ctzll(m);
@@ -830,7 +979,7 @@ __device__ void build_order(const FsmLaunch &L, int *order)
     }
 }
 
-template <typename R, int SLOWMODE, bool FAST>
+template <typename R, int SLOWMODE, bool FAST, int ZSH>
 __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -861,7 +1010,7 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
         for (int t = lane; t < L.ntiles; t += 64) {
             S.lastproc[t] = -1; S.lastchg[t] = -1;       // every tile dirty for the first sweep
-            S.u0ep[t] = 0; S.smallit[t] = 0;
+            S.u0ep[t] = 0;
         }
         BcBoxes bc;
         bc.box = S.box;
@@ -871,20 +1020,21 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
+                const int clock_it = clock;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
                     if (sw & 4)
-                        clock += sweep<R, SLOWMODE, FAST, true>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
+                        clock += sweep<R, SLOWMODE, FAST, true, ZSH>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
                                                                 notconv, ierr_last, visited);
                     else
-                        clock += sweep<R, SLOWMODE, FAST, false>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
+                        clock += sweep<R, SLOWMODE, FAST, false, ZSH>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
                                                                  notconv, ierr_last, visited);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
                 iters = it + 1;
                 if (sweeps_left > 0 || L.max_sweeps < 0) {
-                    if (!__any(notconv)) verify_small<R>(L, ur, u0r, S, it, notconv);
+                    if (!__any(notconv)) verify_small<R>(L, ur, u0r, S, clock_it, notconv);
                     if (!__any(notconv)) break;
                 }
             }
@@ -946,53 +1096,60 @@ __global__ void from_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfiel
 }  // namespace
 
 // ---- host-side launchers (C++ linkage, used by capi.hip) ---------------------
-template <typename R, int SLOWMODE, bool FAST>
+template <typename R, int SLOWMODE, bool FAST, int ZSH>
 static hipError_t launch_fsm(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     size_t lds = fsm_lds_bytes(L, sizeof(R));
-    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST>), dim3(nwaves), dim3(64), lds, st, L);
+    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST, ZSH>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
 }
 
-template <typename R, int SLOWMODE, bool FAST>
+template <typename R, int SLOWMODE, bool FAST, int ZSH>
 static int occupancy_of(size_t lds)
 {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST>, 64, lds) == hipSuccess
-        ? nb : 1;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST, ZSH>, 64, lds) ==
+                   hipSuccess ? nb : 1;
 }
 
-// Kernel variant of a launch: slowness source and sqrt form.
+// Kernel variant of a launch: slowness source, sqrt form, and (cell cache)
+// whether the z refinement is 4 (cell offsets of a brick's slots are constants).
 static int variant(const FsmLaunch &L, int is_double)
 {
-    int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
-    return mode * 2 + (!is_double && mode == 2 && L.fast_sqrt ? 1 : 0);
+    const int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
+    if (is_double) return 8 + mode * 2;
+    if (mode != 2) return mode * 2;
+    return 4 + (L.fast_sqrt ? 1 : 0) + (L.nrz == 4 && L.fast_sqrt ? 2 : 0);
 }
+
+#define FSM_VARIANTS(X)                         \
+    X(0, float, 0, false, -1)                   \
+    X(2, float, 1, false, -1)                   \
+    X(4, float, 2, false, -1)                   \
+    X(5, float, 2, true, -1)                    \
+    X(7, float, 2, true, 2)                     \
+    X(8, double, 0, false, -1)                  \
+    X(10, double, 1, false, -1)                 \
+    X(12, double, 2, false, -1)
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st)
 {
-    switch (variant(L, is_double) + (is_double ? 8 : 0)) {
-    case 0: return launch_fsm<float, 0, false>(L, nwaves, st);
-    case 2: return launch_fsm<float, 1, false>(L, nwaves, st);
-    case 4: return launch_fsm<float, 2, false>(L, nwaves, st);
-    case 5: return launch_fsm<float, 2, true>(L, nwaves, st);
-    case 8: return launch_fsm<double, 0, false>(L, nwaves, st);
-    case 10: return launch_fsm<double, 1, false>(L, nwaves, st);
-    default: return launch_fsm<double, 2, false>(L, nwaves, st);
+    switch (variant(L, is_double)) {
+#define X(v, R, M, F, Z) case v: return launch_fsm<R, M, F, Z>(L, nwaves, st);
+        FSM_VARIANTS(X)
+#undef X
+    default: return hipErrorInvalidValue;
     }
 }
 
 int fsm_occupancy(const FsmLaunch &L, int is_double)
 {
     const size_t lds = fsm_lds_bytes(L, is_double ? 8 : 4);
-    switch (variant(L, is_double) + (is_double ? 8 : 0)) {
-    case 0: return occupancy_of<float, 0, false>(lds);
-    case 2: return occupancy_of<float, 1, false>(lds);
-    case 4: return occupancy_of<float, 2, false>(lds);
-    case 5: return occupancy_of<float, 2, true>(lds);
-    case 8: return occupancy_of<double, 0, false>(lds);
-    case 10: return occupancy_of<double, 1, false>(lds);
-    default: return occupancy_of<double, 2, false>(lds);
+    switch (variant(L, is_double)) {
+#define X(v, R, M, F, Z) case v: return occupancy_of<R, M, F, Z>(lds);
+        FSM_VARIANTS(X)
+#undef X
+    default: return 1;
     }
 }
 
