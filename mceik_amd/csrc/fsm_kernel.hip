@@ -230,11 +230,33 @@ __device__ __forceinline__ double godunov_bl(double a, double b, double c, doubl
     return godunov(a, b, c, f, ierr);   // fp64: the reference's literal form
 }
 
+// Column order inside a brick: the tile perimeter first -- rows ly = 0 and
+// ly = 7 (slots 0..15), then the x faces lx = 0 and lx = 7 (16..27), then the
+// interior -- so each face a neighbour tile reads as its halo spans 2-4
+// 128-B lines instead of 8 (row-major order puts every x-face column in its
+// own line).
+__host__ __device__ __forceinline__ int colpos(int lx, int ly)
+{
+    if (ly == 0) return lx;
+    if (ly == 7) return 8 + lx;
+    if (lx == 0) return 15 + ly;
+    if (lx == 7) return 21 + ly;
+    return 28 + (ly - 1) * 6 + (lx - 1);
+}
+__host__ __device__ __forceinline__ void colpos_inv(int p, int &lx, int &ly)
+{
+    if (p < 8) { lx = p; ly = 0; }
+    else if (p < 16) { lx = p - 8; ly = 7; }
+    else if (p < 22) { lx = 0; ly = p - 15; }
+    else if (p < 28) { lx = 7; ly = p - 21; }
+    else { lx = 1 + (p - 28) % 6; ly = 1 + (p - 28) / 6; }
+}
+
 // x-fastest node -> brick-layout element index
 __device__ __forceinline__ size_t brick_index(const FsmLaunch &L, int x, int y, int z)
 {
     int tile = (y >> 3) * L.ntx + (x >> 3);
-    return ((((size_t)tile * L.nzb + (z >> 3)) * 64 + ((y & 7) * 8 + (x & 7))) << 3) + (z & 7);
+    return ((((size_t)tile * L.nzb + (z >> 3)) * 64 + colpos(x & 7, y & 7)) << 3) + (z & 7);
 }
 
 // Per-solve boundary-condition boxes (EIKONAL3D_SETBCS nodes, lupd = .FALSE.).
@@ -343,16 +365,16 @@ __device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc
     const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
     const int x = tx * 8 + lx, y = ty * 8 + ly;
     const uint32_t es = sizeof(R), st = (uint32_t)L.nzb * 512u;
-    const uint32_t col = ((uint32_t)(ty * L.ntx + tx) * st + (uint32_t)(ly * 8 + lx) * 8u) * es;
+    const uint32_t col = ((uint32_t)(ty * L.ntx + tx) * st + (uint32_t)colpos(lx, ly) * 8u) * es;
     uint32_t hx = OOB, hy = OOB;
     if (lxs == 0 || lxs == 7) {
         const int xn = x + (((lxs == 0) != (rx != 0)) ? -1 : 1);
-        hx = (xn >= 0 && xn < L.nx) ? ((uint32_t)(ty * L.ntx + (xn >> 3)) * st + (uint32_t)(ly * 8 + (xn & 7)) * 8u) * es
+        hx = (xn >= 0 && xn < L.nx) ? ((uint32_t)(ty * L.ntx + (xn >> 3)) * st + (uint32_t)colpos(xn & 7, ly) * 8u) * es
                                      : col;
     }
     if (lys == 0 || lys == 7) {
         const int yn = y + (((lys == 0) != (ry != 0)) ? -1 : 1);
-        hy = (yn >= 0 && yn < L.ny) ? ((uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)((yn & 7) * 8 + lx) * 8u) * es
+        hy = (yn >= 0 && yn < L.ny) ? ((uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)colpos(lx, yn & 7) * 8u) * es
                                      : col;
     }
     int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
@@ -864,7 +886,7 @@ __device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R
             const int x = tx * 8 + lx, y = ty * 8 + ly;
             for (int zb = 0; zb < L.nzb; zb++) {
                 const uint32_t seg = ((uint32_t)id * ((uint32_t)L.nzb * 512u) + (uint32_t)zb * 512u +
-                                      (uint32_t)lane * 8u) * (uint32_t)sizeof(R);
+                                      (uint32_t)colpos(lx, ly) * 8u) * (uint32_t)sizeof(R);
                 R u[8], v0[8];
                 bload8(ur, seg, u);
                 bload8(u0r, seg, v0);
@@ -1073,7 +1095,9 @@ __global__ void to_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfield)
         int col = t & 63; t >>= 6;
         int zb = (int)(t % L.nzb); int tile = (int)(t / L.nzb);
         int ty = tile / L.ntx, tx = tile - ty * L.ntx;
-        int x = tx * 8 + (col & 7), y = ty * 8 + (col >> 3), z = zb * 8 + zi;
+        int clx, cly;
+        colpos_inv(col, clx, cly);
+        int x = tx * 8 + clx, y = ty * 8 + cly, z = zb * 8 + zi;
         RD v = 0;
         if (x < L.nx && y < L.ny && z < L.nz)
             v = (RD)src[fld * (size_t)L.nx * L.ny * L.nz + ((size_t)z * L.ny + y) * L.nx + x];

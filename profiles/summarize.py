@@ -40,7 +40,7 @@ def per_dispatch(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="fsm_solve_kernel<float, 2, true>")
+    ap.add_argument("--kernel", default="fsm_solve_kernel<float, 2, true, 2>")
     ap.add_argument("--workload", default="C3")
     ap.add_argument("--chains", type=int, default=1024)
     ap.add_argument("--source", default="")
