@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v5p"          # bump when the sweep kernel changes; profiles/traffic.json must match
+KERNEL_REV = "fsm-v6"          # bump when the sweep kernel changes; profiles/traffic.json must match
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -160,7 +160,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    fsm_ms, nlaunch, iters, tiles = smp.fsm_stats()
+    fsm_ms, nlaunch, iters, (tiles, segs, segs_changed) = smp.fsm_stats()
     _, logl, nacc, _ = smp.state()
     smp.close()
 
@@ -211,6 +211,7 @@ def main():
                          "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),
                          "iterations_per_solve": round(iters / max(nlaunch, 1) / (per_gpu * p.nstat), 3),
                          "tile_visit_fraction": round(tiles / max(1.0, iters * 8.0 * ntiles), 4),
+                         "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),
                          "full_sweep_equiv_GBs": round(full_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9, 1)},
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),

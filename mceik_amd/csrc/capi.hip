@@ -91,7 +91,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.fast_sqrt = b->fast_sqrt;
     L.niter = b->niter; L.ierr = b->ierr;
     L.iter_total = b->iter_total;
-    L.tile_total = b->tile_total;
+    L.visit_stats = b->visit_stats;
 }
 
 static int g_device_cus = 0;
@@ -534,7 +534,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     rc |= dalloc(s, &d_tt, (size_t)nch * nstat * nev);
     rc |= dalloc(s, &d_niter, (size_t)nch * nstat);
     rc |= dalloc(s, &d_ierr, (size_t)nch * nstat);
-    rc |= dalloc(s, &s->d_iters, 2);          // [0] iterations, [1] tile visits
+    rc |= dalloc(s, &s->d_iters, 4);          // [0] iterations, [1..3] visit_stats
     if (s->max_samples) {
         rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncell);
         rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
@@ -552,7 +552,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = d_ierr;
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
-    b.tile_total = s->d_iters + 1;
+    b.visit_stats = s->d_iters + 1;
     b.fast_sqrt = parms->dx / (double)o->vmax >= 1e-12 ? 1 : 0;   // f = h/v stays a normal float
     s->ws_bytes = mceik_fsm_workspace_bytes(&b);
     if (hipMalloc(&s->ws, s->ws_bytes) != hipSuccess) {
@@ -565,7 +565,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         mceik_mcmc_finalize(&s);
         return -1;
     }
-    hipMemset(s->d_iters, 0, 2 * sizeof(unsigned long long));
+    hipMemset(s->d_iters, 0, 4 * sizeof(unsigned long long));
     *out = s;
     return 0;
 }
@@ -639,7 +639,7 @@ extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **ni
 }
 
 extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsigned long long *iters,
-                                    unsigned long long *tiles, int reset)
+                                    unsigned long long *visits, int reset)
 {
     if (!s) return 1;
     HIPCHK(hipStreamSynchronize(s->stream));
@@ -649,16 +649,16 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
         HIPCHK(hipEventElapsedTime(&t, s->ev[i], s->ev[i + 1]));
         ms += t;
     }
-    unsigned long long it[2] = {0, 0};
+    unsigned long long it[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpy(it, s->d_iters, sizeof(it), hipMemcpyDeviceToHost));
     if (fsm_ms) *fsm_ms = ms;
     if (nlaunch) *nlaunch = s->nlaunch;
     if (iters) *iters = it[0];
-    if (tiles) *tiles = it[1];
+    if (visits) { visits[0] = it[1]; visits[1] = it[2]; visits[2] = it[3]; }
     if (reset) {
         s->ev_used = 0;
         s->nlaunch = 0;
-        HIPCHK(hipMemset(s->d_iters, 0, 2 * sizeof(unsigned long long)));
+        HIPCHK(hipMemset(s->d_iters, 0, 4 * sizeof(unsigned long long)));
     }
     return 0;
 }

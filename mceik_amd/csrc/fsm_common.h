@@ -37,7 +37,7 @@ struct FsmLaunch {
     int fast_sqrt;               // host-validated: f = s*h is a normal float >= 1e-18
     unsigned *counter;           // 8 work-queue heads, 128 B apart (zeroed before the launch)
     unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
-    unsigned long long *tile_total;   // += tile visits (one tile x nzb bricks, one sweep), may be null
+    unsigned long long *visit_stats;  // [3] += tile visits, column-segment updates, changed segments; may be null
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }

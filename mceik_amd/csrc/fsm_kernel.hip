@@ -33,37 +33,9 @@ template <> struct Num<double> {
 };
 
 // ---- the Godunov local solve ------------------------------------------------
-// fp32: cancellation-free form (increments relative to a1), bitwise equal to
-// oracle/fsm_impl.inc STABLE_UPDATE.  fp64: the reference's literal
-// SOLVE_HAMILTONIAN2D/3D (fsm3d.f90:624-693).
-__device__ __forceinline__ float godunov(float a, float b, float c, float f, int &ierr)
-{
-    const float UN = FLT_MAX;
-    float lo = a < b ? a : b, hi = a < b ? b : a;
-    float a1 = lo < c ? lo : c;
-    float a3 = hi < c ? c : hi;
-    float a2 = lo < c ? (hi < c ? hi : c) : lo;
-    ierr = 0;
-    if (a1 == UN) return UN;
-    float d2 = a2 - a1, d3 = a3 - a1, y;
-    if (!(f > d2)) {
-        y = f;
-    } else {
-        y = 0.5f * (d2 + __builtin_sqrtf((2.0f * f) * f - d2 * d2));
-        if (y > d3) {
-            float sm = d2 + d3;
-            float q = ((d2 * d2) + (d3 * d3)) - f * f;
-            float disc = sm * sm - 3.0f * q;
-            if (disc < 0.0f) ierr = 1;
-            y = (sm + __builtin_sqrtf(disc)) * (1.0f / 3.0f);
-        }
-    }
-    float x = a1 + y;
-    if (x < UN) return x;
-    ierr = 3;
-    return UN;
-}
-
+// fp64: the reference's literal SOLVE_HAMILTONIAN2D/3D (fsm3d.f90:624-693).
+// fp32: godunov_bl / godunov_v below, bitwise equal to oracle/fsm_impl.inc
+// STABLE_UPDATE (increments relative to a1, one square root per solve).
 __device__ __forceinline__ double godunov(double a, double b, double c, double f, int &ierr)
 {
     const double UN = DBL_MAX;
@@ -187,7 +159,9 @@ __device__ __forceinline__ double bperm(int addr, double v)
 // Correctly rounded sqrt for normal positive x (LLVM's expansion without the
 // denormal rescale and zero/inf fix-up).  Used only where the radicand that
 // is finally selected is provably a normal float: on the MCMC path f = h*s >=
-// h/vmax (checked on the host) and both radicands are then >= f^2 / 3.
+// h/vmax (checked on the host) and the selected radicand exceeds f^2 (2D:
+// 2f^2 - d2^2 with d2 < f; 3D: 3f^2 - d2^2 - (d3^2 + (d3-d2)^2) with both
+// terms < f^2).
 __device__ __forceinline__ float sqrt_normal(float x)
 {
     const float s = __builtin_amdgcn_sqrtf(x);
@@ -199,9 +173,10 @@ __device__ __forceinline__ float sqrt_normal(float x)
     return eup > 0.0f ? up : t;
 }
 
-// Branchless fp32 Godunov update (values and ierr identical to godunov(float)
-// above and to the twin): the 2D and 3D candidates are evaluated side by side,
-// so the two correctly rounded square roots are not serialised.
+// Branchless fp32 Godunov update, values and ierr identical to the twin
+// (oracle/fsm_impl.inc STABLE_UPDATE): 1D if f <= d2, else the 2D root unless
+// d3^2 + (d3 - d2)^2 < f^2 (the 2D root would exceed d3), then the 3D root;
+// only the selected radicand is square-rooted.
 template <bool FAST>
 __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, int &ierr)
 {
@@ -210,14 +185,18 @@ __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, 
     const float a3 = fmaxf(fmaxf(a, b), c);
     const float a2 = __builtin_amdgcn_fmed3f(a, b, c);
     const float d2 = a2 - a1, d3 = a3 - a1;
-    const float r2 = (2.0f * f) * f - d2 * d2;
-    const float y2 = 0.5f * (d2 + (FAST ? sqrt_normal(r2) : __builtin_sqrtf(r2)));
+    const float ff = f * f, e = d3 - d2;
+    const float d22 = d2 * d2, d33 = d3 * d3;
+    const bool two = (d33 + e * e) >= ff;
+    const float r2 = (ff + ff) - d22;
     const float sm = d2 + d3;
-    const float q = ((d2 * d2) + (d3 * d3)) - f * f;
+    const float q = (d22 + d33) - ff;
     const float disc = sm * sm - 3.0f * q;
-    const float y3 = (sm + (FAST ? sqrt_normal(disc) : __builtin_sqrtf(disc))) * (1.0f / 3.0f);
-    const bool one = !(f > d2), two = !(y2 > d3);
-    const float y = one ? f : (two ? y2 : y3);
+    const float rad = two ? r2 : disc;
+    const float s = FAST ? sqrt_normal(rad) : __builtin_sqrtf(rad);
+    const float y23 = two ? 0.5f * (d2 + s) : (sm + s) * (1.0f / 3.0f);
+    const bool one = !(f > d2);
+    const float y = one ? f : y23;
     const float x = a1 + y;
     const bool ok = x < UN;
     const bool nan_in = a1 == UN;
@@ -601,13 +580,16 @@ __device__ __forceinline__ float godunov_v(float a, float b, float c, float f)
     const float a3 = __builtin_bit_cast(float, __builtin_elementwise_max(hi, ic));
     const float a2 = __builtin_bit_cast(float, __builtin_elementwise_max(lo, __builtin_elementwise_min(hi, ic)));
     const float d2 = a2 - a1, d3 = a3 - a1;
-    const float r2 = (2.0f * f) * f - d2 * d2;
-    const float y2 = 0.5f * (d2 + (FAST ? sqrt_normal(r2) : __builtin_sqrtf(r2)));
+    const float ff = f * f, e = d3 - d2;
+    const float d22 = d2 * d2, d33 = d3 * d3;
+    const bool two = (d33 + e * e) >= ff;
+    const float r2 = (ff + ff) - d22;
     const float sm = d2 + d3;
-    const float q = ((d2 * d2) + (d3 * d3)) - f * f;
+    const float q = (d22 + d33) - ff;
     const float disc = sm * sm - 3.0f * q;
-    const float y3 = (sm + (FAST ? sqrt_normal(disc) : __builtin_sqrtf(disc))) * (1.0f / 3.0f);
-    const float y = !(f > d2) ? f : (!(y2 > d3) ? y2 : y3);
+    const float s = FAST ? sqrt_normal(two ? r2 : disc) : __builtin_sqrtf(two ? r2 : disc);
+    const float y23 = two ? 0.5f * (d2 + s) : (sm + s) * (1.0f / 3.0f);
+    const float y = !(f > d2) ? f : y23;
     // x >= UN, +inf or NaN -> UN: unsigned min with the bits of FLT_MAX (x >= +0)
     const unsigned ix = __builtin_bit_cast(unsigned, a1 + y);
     return __builtin_bit_cast(float, __builtin_elementwise_min(ix, 0x7f7fffffu));
@@ -725,7 +707,8 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
                                      const Smem<R> &S, int rx, int ry, int it, int clock0,
-                                     bool &notconv, int &ierr_last, unsigned long long &visited)
+                                     bool &notconv, int &ierr_last, unsigned long long &visited,
+                                     unsigned long long &segs, unsigned long long &segs_changed)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
@@ -823,6 +806,15 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         const bool val = (b0.fl & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
+        if (L.visit_stats) {                                // wave-uniform; SALU popcounts
+            segs += __builtin_popcountll(__ballot(val && (b0.fl & C_ACT)));
+#ifdef MCEIK_BRICK_STATS
+            // debug: count changed BRICKS (lanes of one brick share d = lxs + lys)
+            for (int dd = 0; dd < 15; dd++) segs_changed += __ballot(changed && d == dd) != 0;
+#else
+            segs_changed += __builtin_popcountll(__ballot(changed));
+#endif
+        }
 
         // ---- write-back, u0 at a tile's first visit of the iteration, change stamps
         bstore8(ur, changed ? b0.seg : OOB, r);
@@ -1009,7 +1001,7 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
     build_order(L, S.order);
-    unsigned long long visited = 0;
+    unsigned long long visited = 0, segs = 0, segs_changed = 0;
     int pass = 0;
     for (;;) {
         const int snext = next_solve(L, pass);
@@ -1047,10 +1039,10 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
                     if (sw & 4)
                         clock += sweep<R, SLOWMODE, FAST, true, ZSH>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
-                                                                notconv, ierr_last, visited);
+                                                                notconv, ierr_last, visited, segs, segs_changed);
                     else
                         clock += sweep<R, SLOWMODE, FAST, false, ZSH>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
-                                                                 notconv, ierr_last, visited);
+                                                                 notconv, ierr_last, visited, segs, segs_changed);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
@@ -1081,7 +1073,11 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
-    if (lane == 0 && L.tile_total && visited) atomicAdd(L.tile_total, visited);
+    if (lane == 0 && L.visit_stats) {
+        atomicAdd(L.visit_stats, visited);
+        atomicAdd(L.visit_stats + 1, segs);
+        atomicAdd(L.visit_stats + 2, segs_changed);
+    }
 }
 
 // ---- layout conversion (x-fastest <-> brick), drop-in entry points only ----
