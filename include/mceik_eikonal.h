@@ -63,8 +63,9 @@ typedef struct mceik_fsm_batch {
     unsigned long long *iter_total;  /* device counter += iterations of every solve, or NULL */
     int fast_sqrt;              /* 1: caller guarantees h*slowness >= 1e-12 (cells mode, fp32):
                                    use the shorter correctly rounded sqrt (same results) */
-    unsigned long long *tile_total;  /* device counter += tile visits (8x8 columns x nz, one sweep),
-                                        or NULL; tiles whose inputs did not change are skipped */
+    unsigned long long *visit_stats; /* device [3] += tile visits (8x8 columns x nz, one sweep; tiles
+                                        whose inputs did not change are skipped), column segments
+                                        (8 nodes) updated, segments that changed; or NULL */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */
