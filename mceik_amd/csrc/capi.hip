@@ -62,7 +62,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
 {
     memset(&L, 0, sizeof(L));
     L.nx = b->nx; L.ny = b->ny; L.nz = b->nz;
-    fsm_geometry(&L);
+    fsm_geometry(&L, b->precision == 64 ? 8 : 4);
     L.maxit = b->maxit; L.max_sweeps = b->max_sweeps;
     L.tol = b->tol; L.h = b->h; L.x0 = b->x0; L.y0 = b->y0; L.z0 = b->z0;
     int is_double = b->precision == 64;

@@ -24,7 +24,8 @@ struct FsmLaunch {
     const void *slow;            // mode 0: [nmodel][field_elems] R ; mode 1: [nmodel][ncell] float
     int ncx, ncy, ncz, nrx, nry, nrz;
     unsigned magic_rx, magic_ry, magic_rz;   // ceil(2^20 / nr*): cell = (node * magic) >> 20
-    size_t field_elems;          // ntiles * nzb * 512
+    int nzq;                     // 128-B line groups per column: ceil(nzb / (16 / es))
+    size_t field_elems;          // ntiles * nzq * 64 * (128 / es)
     void *u;                     // travel-time fields (brick layout, R)
     void *u0;                    // convergence side field (same layout)
     int slot_per_solve;          // 1: field slot = solve id; 0: slot = blockIdx.x (scratch)
@@ -77,13 +78,17 @@ static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
 }
 #define MCEIK_MAX_LDS (64 * 1024)   // dynamic LDS without a launch attribute
 
-// Fills the tile geometry of a launch from nx, ny, nz.
-static inline void fsm_geometry(FsmLaunch *L)
+// Fills the tile geometry of a launch from nx, ny, nz (es: element bytes).
+// Field layout: per 8x8 column tile, z-major groups of one
+// 128-B line per column (32 fp32 / 16 fp64 z values), columns in colpos order.
+static inline void fsm_geometry(FsmLaunch *L, int es)
 {
     L->ntx = mceik_div_up(L->nx, MCEIK_TILE);
     L->nty = mceik_div_up(L->ny, MCEIK_TILE);
     L->nzb = mceik_div_up(L->nz, MCEIK_TILE);
     L->sb = L->nzb > MCEIK_MIN_SB ? L->nzb : MCEIK_MIN_SB;
     L->ntiles = L->ntx * L->nty;
-    L->field_elems = (size_t)L->ntiles * L->nzb * MCEIK_BRICK;
+    const int bpl = 16 / es;                     // 8-z bricks per 128-B line
+    L->nzq = mceik_div_up(L->nzb, bpl);
+    L->field_elems = (size_t)L->ntiles * L->nzq * 64 * (128 / es);
 }

@@ -231,11 +231,31 @@ __host__ __device__ __forceinline__ void colpos_inv(int p, int &lx, int &ly)
     else { lx = 1 + (p - 28) % 6; ly = 1 + (p - 28) / 6; }
 }
 
-// x-fastest node -> brick-layout element index
+// Field layout: per tile, groups of 128-B lines, one per column (colpos
+// order), each holding ZQ = 128/es consecutive z of that column.  A lane
+// reads and writes its 8-z segment of a line in BPL consecutive steps, so a
+// line is fetched once per tile visit (a row-of-bricks layout spreads each
+// line over 4 columns that different lane diagonals reach up to 14 steps
+// apart, and the L2 refetches it).
+template <typename R> struct Lay {
+    static constexpr int ZQ = 128 / (int)sizeof(R);      // z per line
+    static constexpr int BPL = ZQ / 8;                   // 8-z bricks per line
+};
+template <typename R>
+__device__ __forceinline__ uint32_t zoff_bytes(int zb)
+{
+    return (uint32_t)(zb / Lay<R>::BPL) * 8192u + (uint32_t)(zb % Lay<R>::BPL) * 8u * (uint32_t)sizeof(R);
+}
+template <typename R>
+__device__ __forceinline__ uint32_t tile_bytes(const FsmLaunch &L) { return (uint32_t)L.nzq * 8192u; }
+
+// x-fastest node -> field element index
+template <typename R>
 __device__ __forceinline__ size_t brick_index(const FsmLaunch &L, int x, int y, int z)
 {
-    int tile = (y >> 3) * L.ntx + (x >> 3);
-    return ((((size_t)tile * L.nzb + (z >> 3)) * 64 + colpos(x & 7, y & 7)) << 3) + (z & 7);
+    constexpr int ZQ = Lay<R>::ZQ;
+    const int tile = (y >> 3) * L.ntx + (x >> 3);
+    return (((size_t)tile * L.nzq + z / ZQ) * 64 + colpos(x & 7, y & 7)) * ZQ + z % ZQ;
 }
 
 // Per-solve boundary-condition boxes (EIKONAL3D_SETBCS nodes, lupd = .FALSE.).
@@ -343,17 +363,17 @@ __device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc
 {
     const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
     const int x = tx * 8 + lx, y = ty * 8 + ly;
-    const uint32_t es = sizeof(R), st = (uint32_t)L.nzb * 512u;
-    const uint32_t col = ((uint32_t)(ty * L.ntx + tx) * st + (uint32_t)colpos(lx, ly) * 8u) * es;
+    const uint32_t st = tile_bytes<R>(L);
+    const uint32_t col = (uint32_t)(ty * L.ntx + tx) * st + (uint32_t)colpos(lx, ly) * 128u;
     uint32_t hx = OOB, hy = OOB;
     if (lxs == 0 || lxs == 7) {
         const int xn = x + (((lxs == 0) != (rx != 0)) ? -1 : 1);
-        hx = (xn >= 0 && xn < L.nx) ? ((uint32_t)(ty * L.ntx + (xn >> 3)) * st + (uint32_t)colpos(xn & 7, ly) * 8u) * es
+        hx = (xn >= 0 && xn < L.nx) ? (uint32_t)(ty * L.ntx + (xn >> 3)) * st + (uint32_t)colpos(xn & 7, ly) * 128u
                                      : col;
     }
     if (lys == 0 || lys == 7) {
         const int yn = y + (((lys == 0) != (ry != 0)) ? -1 : 1);
-        hy = (yn >= 0 && yn < L.ny) ? ((uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)colpos(lx, yn & 7) * 8u) * es
+        hy = (yn >= 0 && yn < L.ny) ? (uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)colpos(lx, yn & 7) * 128u
                                      : col;
     }
     int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
@@ -385,7 +405,7 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
     const bool valid = pos_valid(p, nstream, L.nzb);
     const u4v ci = S.cinfo[(p.sp & 3) * 64 + lane];
     const int zb = valid ? (RZ ? L.nzb - 1 - p.zbs : p.zbs) : 0;
-    const uint32_t zoff = (uint32_t)zb * 512u * (uint32_t)sizeof(R);
+    const uint32_t zoff = zoff_bytes<R>(zb);
     b.seg = valid ? ci.x + zoff : OOB;
     b.hx = valid ? ci.y + zoff : OOB;
     b.hy = valid ? ci.z + zoff : OOB;
@@ -425,7 +445,7 @@ template <typename R, int SLOWMODE>
 __device__ __forceinline__ double slow_at(const FsmLaunch &L, const void *slow_model, int x, int y, int z)
 {
     if (SLOWMODE == 0)
-        return (double)reinterpret_cast<const R *>(slow_model)[brick_index(L, x, y, z)];   // modes 1, 2: cells
+        return (double)reinterpret_cast<const R *>(slow_model)[brick_index<R>(L, x, y, z)];   // modes 1, 2: cells
     const float *si = reinterpret_cast<const float *>(slow_model);
     return (double)si[((size_t)(z / L.nrz) * L.ncy + y / L.nry) * L.ncx + x / L.nrx];
 }
@@ -789,7 +809,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             const bool v2 = pos_valid(p2, nstream, L.nzb);
             const uint32_t col2 = S.cinfo[(p2.sp & 3) * 64 + lane].x;
             const int zb2 = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
-            bload8(ur, v2 ? col2 + (uint32_t)zb2 * 512u * (uint32_t)sizeof(R) : OOB, q);
+            bload8(ur, v2 ? col2 + zoff_bytes<R>(zb2) : OOB, q);
         }
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
         bload8(ur, b1.hx, hxq);
@@ -877,8 +897,7 @@ __device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R
             const int tx = id % L.ntx, ty = id / L.ntx;
             const int x = tx * 8 + lx, y = ty * 8 + ly;
             for (int zb = 0; zb < L.nzb; zb++) {
-                const uint32_t seg = ((uint32_t)id * ((uint32_t)L.nzb * 512u) + (uint32_t)zb * 512u +
-                                      (uint32_t)colpos(lx, ly) * 8u) * (uint32_t)sizeof(R);
+                const uint32_t seg = (uint32_t)id * tile_bytes<R>(L) + zoff_bytes<R>(zb) + (uint32_t)colpos(lx, ly) * 128u;
                 R u[8], v0[8];
                 bload8(ur, seg, u);
                 bload8(u0r, seg, v0);
@@ -948,7 +967,7 @@ __device__ bool init_field(const FsmLaunch &L, R *u, Rsrc ur, const void *slow_m
                 double dd = __builtin_sqrt((ddx * ddx + ddy * ddy) + ddz * ddz);
                 double sl = slow_at<R, SLOWMODE>(L, slow_model, ix - 1, iy - 1, iz - 1);
                 R t = (R)(ts + dd * sl);
-                size_t idx = brick_index(L, ix - 1, iy - 1, iz - 1);
+                size_t idx = brick_index<R>(L, ix - 1, iy - 1, iz - 1);
                 R cur = u[idx];
                 u[idx] = (__builtin_fabs(dd) < 1.e-10) ? t : (cur < t ? cur : t);
             }
@@ -1067,7 +1086,7 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                 int node = L.ev_node[e];
                 int nxy = L.nx * L.ny;
                 int z = node / nxy, rem = node - z * nxy, y = rem / L.nx, x = rem - y * L.nx;
-                L.ttab[(size_t)solve * L.nev + e] = (float)u[brick_index(L, x, y, z)];
+                L.ttab[(size_t)solve * L.nev + e] = (float)u[brick_index<R>(L, x, y, z)];
             }
         }
         __builtin_amdgcn_s_waitcnt(0);
@@ -1087,13 +1106,15 @@ __global__ void to_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfield)
     size_t n = L.field_elems * (size_t)nfield;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         size_t fld = i / L.field_elems, e = i - fld * L.field_elems;
-        int zi = e & 7; size_t t = e >> 3;
-        int col = t & 63; t >>= 6;
-        int zb = (int)(t % L.nzb); int tile = (int)(t / L.nzb);
+        constexpr int ZQ = Lay<RD>::ZQ;                   // destination layout (brick_index<RD>)
+        const int zi = (int)(e % ZQ);
+        size_t t = e / ZQ;
+        const int col = (int)(t & 63); t >>= 6;
+        const int zq = (int)(t % L.nzq); const int tile = (int)(t / L.nzq);
         int ty = tile / L.ntx, tx = tile - ty * L.ntx;
         int clx, cly;
         colpos_inv(col, clx, cly);
-        int x = tx * 8 + clx, y = ty * 8 + cly, z = zb * 8 + zi;
+        int x = tx * 8 + clx, y = ty * 8 + cly, z = zq * ZQ + zi;
         RD v = 0;
         if (x < L.nx && y < L.ny && z < L.nz)
             v = (RD)src[fld * (size_t)L.nx * L.ny * L.nz + ((size_t)z * L.ny + y) * L.nx + x];
@@ -1109,7 +1130,7 @@ __global__ void from_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfiel
         size_t fld = i / nn, e = i - fld * nn;
         int x = (int)(e % L.nx); size_t t = e / L.nx;
         int y = (int)(t % L.ny); int z = (int)(t / L.ny);
-        dst[i] = (RD)src[fld * L.field_elems + brick_index(L, x, y, z)];
+        dst[i] = (RD)src[fld * L.field_elems + brick_index<RS>(L, x, y, z)];
     }
 }
 
