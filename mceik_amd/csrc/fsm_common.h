@@ -9,7 +9,7 @@
 #define MCEIK_MAX_SRC 8          // point sources per solve (box BCs, fsm3d.f90:762-840)
 #define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
 #define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
-#define MCEIK_MIN_SB 11          // virtual bricks per tile (>= nzb); halo lags need >= 11
+#define MCEIK_MIN_SB 12          // virtual bricks per tile (>= nzb); halo lags need >= 12
 
 // One batched launch: nsolve = nmodel * nstat solves; solve id = model*nstat + station.
 struct FsmLaunch {

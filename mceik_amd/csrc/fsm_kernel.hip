@@ -340,7 +340,7 @@ enum {
 
 // What a lane needs about one of its bricks.
 struct BInfo {
-    uint32_t seg, hx, hy;    // byte offsets (u buffer): own segment, x halo, y halo (OOB if none)
+    uint32_t seg;            // byte offset (u buffer) of the own segment (OOB if none)
     int zb8, fl, ccb, sp;    // fl: C_* | F_*; ccb: cell-cache index of the brick (SLOWMODE 2)
     int bcm;                 // BC z-slots of the segment (generic path)
 };
@@ -407,8 +407,6 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
     const int zb = valid ? (RZ ? L.nzb - 1 - p.zbs : p.zbs) : 0;
     const uint32_t zoff = zoff_bytes<R>(zb);
     b.seg = valid ? ci.x + zoff : OOB;
-    b.hx = valid ? ci.y + zoff : OOB;
-    b.hy = valid ? ci.z + zoff : OOB;
     b.zb8 = zb * 8;
     b.sp = p.sp;
     const int meta = (int)ci.w;
@@ -439,6 +437,19 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
     b.fl = fl;
     b.ccb = (meta >> 8) + (ZSH >= 0 ? (b.zb8 >> (ZSH < 0 ? 0 : ZSH)) : 0);
     return b;
+}
+
+// Offsets of lane col_lane's segment and halos at stream position p (prefetch).
+template <typename R, bool RZ>
+__device__ __forceinline__ void seg_offsets(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
+                                            uint32_t &seg, uint32_t &hx, uint32_t &hy, int col_lane)
+{
+    const bool valid = pos_valid(p, nstream, L.nzb);
+    const u4v ci = S.cinfo[(p.sp & 3) * 64 + col_lane];
+    const uint32_t zoff = zoff_bytes<R>(RZ ? L.nzb - 1 - p.zbs : p.zbs);
+    seg = valid ? ci.x + zoff : OOB;
+    hx = valid ? ci.y + zoff : OOB;
+    hy = valid ? ci.z + zoff : OOB;
 }
 
 template <typename R, int SLOWMODE>
@@ -621,6 +632,47 @@ __device__ __forceinline__ double godunov_v(double a, double b, double c, double
     return godunov(a, b, c, f, e);
 }
 
+// x/y neighbour minima and f = s*h of slot pj.  The x and y neighbours come
+// from the other lanes' r (updated in their previous step) and n, which the
+// current step does not modify, so any slot may gather them at any time.
+template <typename R, int SLOWMODE, int ZSH, bool GENERIC>
+__device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, const R (&c)[8],
+                                          const R (&n)[8], const R (&r)[8], int pj, int aup, int adn,
+                                          bool xp, bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
+{
+    const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3;
+    const int hxsel = lxs == 7, hysel = lys >= 4;
+    const R self = c[pj];
+    const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
+    const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
+    if (SLOWMODE == 2) {
+        if (ZSH >= 0 && !GENERIC) {
+            fv = (R)S.cc[b0.ccb + (pj >> (ZSH < 0 ? 0 : ZSH))];
+        } else {
+            const int zabs = b0.zb8 + pj;
+            fv = (R)S.cc[b0.ccb + (ZSH >= 0 ? (pj >> (ZSH < 0 ? 0 : ZSH))
+                                            : (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20))];
+        }
+        if (sizeof(R) == 8) fv *= (R)L.h;        // fp32 entries already hold s*h
+    } else {
+        fv = S.sf[pj * 64 + lane];
+    }
+    R hxv = S.shx[(pj * 2 + hxsel) * 8 + lys];
+    R hyv = S.shy[(pj * 2 + hysel) * 8 + lxs];
+    // keep the LDS reads unconditional (hipcc otherwise sinks them into
+    // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
+    asm volatile("" : "+v"(hxv), "+v"(hyv));
+    R xup = lxs > 0 ? xm : hxv;
+    R xdn = lxs < 7 ? xpv : hxv;
+    R yup = lys > 0 ? ym : hyv;
+    R ydn = lys < 7 ? ypv : hyv;
+    if (GENERIC) {
+        xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
+    }
+    ux = fmin_(xup, xdn);
+    uy = fmin_(yup, ydn);
+}
+
 // The 8 z-slots of the current brick.  GENERIC: any brick (grid-edge columns
 // of cut tiles, cut z-bricks, BC nodes, node (0,0,0) with the reference's
 // ierr); otherwise the brick is interior to the grid in x, y and z up to the
@@ -631,9 +683,8 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
                                              R (&n)[8], R (&r)[8], int lx, int ly, int rx, int ry,
                                              bool &changed, bool &nc, int &ierr_last)
 {
-    const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3;
-    const int hxsel = lxs == 7, hysel = lys >= 4;
-    const R hr = (R)L.h, T = (R)L.conv_thresh;
+    const int lane = threadIdx.x;
+    const R T = (R)L.conv_thresh;
     const int fl = b0.fl;
     bool xp = true, xn = true, yp = true, yn = true, act = true;
     if (GENERIC) {
@@ -646,51 +697,14 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
     const bool first = (fl & F_FIRST) != 0, last = (fl & F_LAST) != 0;
     int aup = ((lane - 8) & 63) * 4, adn = ((lane + 8) & 63) * 4;
     asm volatile("" : "+v"(aup), "+v"(adn));
-    // x and y neighbours of all 8 slots first: they come from the other lanes'
-    // r (updated in their previous step) and n, which this step does not
-    // modify, so the 16 lane exchanges and the LDS reads overlap.
-    R ux[8], uy[8], fvs[8];
-#pragma unroll
-    for (int pj = 0; pj < 8; pj++) {
-        const R self = c[pj];
-        const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
-        const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
-        R fv;
-        if (SLOWMODE == 2) {
-            if (ZSH >= 0 && !GENERIC) {
-                fv = (R)S.cc[b0.ccb + (pj >> (ZSH < 0 ? 0 : ZSH))];
-            } else {
-                const int zabs = b0.zb8 + pj;
-                fv = (R)S.cc[b0.ccb + (ZSH >= 0 ? (pj >> (ZSH < 0 ? 0 : ZSH))
-                                                : (int)(((unsigned)(zabs < L.nz ? zabs : L.nz - 1) * L.magic_rz) >> 20))];
-            }
-            if (sizeof(R) == 8) fv *= hr;         // fp32 entries already hold s*h
-        } else {
-            fv = S.sf[pj * 64 + lane];
-        }
-        R hxv = S.shx[(pj * 2 + hxsel) * 8 + lys];
-        R hyv = S.shy[(pj * 2 + hysel) * 8 + lxs];
-        // keep the LDS reads unconditional (hipcc otherwise sinks them into
-        // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
-        asm volatile("" : "+v"(hxv), "+v"(hyv));
-        R xup = lxs > 0 ? xm : hxv;
-        R xdn = lxs < 7 ? xpv : hxv;
-        R yup = lys > 0 ? ym : hyv;
-        R ydn = lys < 7 ? ypv : hyv;
-        if (GENERIC) {
-            xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
-        }
-        ux[pj] = fmin_(xup, xdn);
-        uy[pj] = fmin_(yup, ydn);
-        fvs[pj] = fv;
-    }
-    // then the z chain in sweep order
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const int pj = RZ ? 7 - j : j;
         const int pprev = RZ ? pj + 1 : pj - 1;
         const int pnext = RZ ? pj - 1 : pj + 1;
         const R self = c[pj];
+        R ux, uy, fv;
+        gather_xy<R, SLOWMODE, ZSH, GENERIC>(L, S, b0, c, n, r, pj, aup, adn, xp, xn, yp, yn, ux, uy, fv);
         R zup, zdn;
         if (GENERIC) {
             const int zabs = b0.zb8 + pj;
@@ -707,12 +721,12 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
         if (GENERIC) {
             const int zabs = b0.zb8 + pj;
             int e;
-            const R ub = godunov_bl<FAST>(ux[pj], uy[pj], uz, fvs[pj], e);
+            const R ub = godunov_bl<FAST>(ux, uy, uz, fv, e);
             const bool upd = act && zabs < L.nz && !((b0.bcm >> pj) & 1);
             nv = upd ? fmin_(self, ub) : self;
             if ((fl & C_00) && zabs == 0) ierr_last = upd ? e : 0;
         } else {
-            nv = fmin_(self, godunov_v<FAST>(ux[pj], uy[pj], uz, fvs[pj]));
+            nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv));
         }
         const bool dec = nv < self;
         nc |= dec && self >= T;
@@ -735,6 +749,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     const R UN = Num<R>::unan();
     const R hr = (R)L.h, T = (R)L.conv_thresh;
     const int sb = L.sb;
+
     const int hxsel = lxs == 7, hysel = lys >= 4;
 
     // stream bookkeeping (wave-uniform)
@@ -745,7 +760,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         admit_tile<R>(L, S, bc, e, 0, clock0, it, lx, ly, lxs, lys, rx, ry);
         ndecided = 1;
     }
-    R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8];
+    R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8], hxn[8], hyn[8];
     float ccv[CC_MAX / 64];
     int ccsize = 0;
     Pos p1;
@@ -759,12 +774,19 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     } else {
         prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
     }
-    bload8(ur, b0.hx, hxq);
-    bload8(ur, b0.hy, hyq);
+    {
+        uint32_t s_, hx_, hy_;
+        seg_offsets<R, RZ>(L, S, p1, nstream, s_, hx_, hy_, lane);
+        bload8(ur, hx_, hxq);
+        bload8(ur, hy_, hyq);
+    }
     pos_adv(p1, sb);
     {
-        BInfo b1 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
-        bload8(ur, b1.seg, n);
+        uint32_t s1, hx_, hy_;
+        seg_offsets<R, RZ>(L, S, p1, nstream, s1, hx_, hy_, lane);
+        bload8(ur, s1, n);
+        bload8(ur, hx_, hxn);            // halos of vb+1: one more step in flight
+        bload8(ur, hy_, hyn);
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -779,6 +801,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #pragma unroll
         for (int i = 0; i < 8; i++) S.shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
     }
+#pragma unroll
+    for (int i = 0; i < 8; i++) { hxq[i] = hxn[i]; hyq[i] = hyn[i]; }
     asm volatile("" ::: "memory");
 
     int ph = 2 % sb;                 // (B + 2) mod sb: 0 when lane (0,0)'s vb+2 starts a new position
@@ -801,19 +825,20 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             }
         }
         if (nstream != 0x7fffffff && B >= nstream * sb + 14) break;
-        // ---- prefetch: u of vb+2 (-> n next step); slowness and halos of vb+1
+        // ---- prefetch: own segment and halos of vb+2 (halos are staged at
+        // the end of the next step: two steps of latency cover, MCEIK_MIN_SB
+        // = 12), slowness of vb+1
         const BInfo b1 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
         {
             Pos p2 = p1;
             pos_adv(p2, sb);
-            const bool v2 = pos_valid(p2, nstream, L.nzb);
-            const uint32_t col2 = S.cinfo[(p2.sp & 3) * 64 + lane].x;
-            const int zb2 = RZ ? L.nzb - 1 - p2.zbs : p2.zbs;
-            bload8(ur, v2 ? col2 + zoff_bytes<R>(zb2) : OOB, q);
+            uint32_t s2, hx_, hy_;
+            seg_offsets<R, RZ>(L, S, p2, nstream, s2, hx_, hy_, lane);
+            bload8(ur, s2, q);
+            bload8(ur, hx_, hxn);
+            bload8(ur, hy_, hyn);
         }
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
-        bload8(ur, b1.hx, hxq);
-        bload8(ur, b1.hy, hyq);
 
         // ---- the 8 z-slots of the current brick
         bool changed = false, nc = false;
@@ -828,12 +853,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         notconv |= nc && val;
         if (L.visit_stats) {                                // wave-uniform; SALU popcounts
             segs += __builtin_popcountll(__ballot(val && (b0.fl & C_ACT)));
-#ifdef MCEIK_BRICK_STATS
-            // debug: count changed BRICKS (lanes of one brick share d = lxs + lys)
-            for (int dd = 0; dd < 15; dd++) segs_changed += __ballot(changed && d == dd) != 0;
-#else
             segs_changed += __builtin_popcountll(__ballot(changed));
-#endif
         }
 
         // ---- write-back, u0 at a tile's first visit of the iteration, change stamps
@@ -870,7 +890,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; }
+        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; hxq[i] = hxn[i]; hyq[i] = hyn[i]; }
         b0 = b1;
         pos_adv(p1, sb);
         if (++ph == sb) ph = 0;
