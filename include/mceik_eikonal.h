@@ -41,6 +41,35 @@ int locate_l2_gridSearch__double64(int ldgrd, int ngrd, int nobs, int iwantOT, d
                                    const double *varobs, const double *test,
                                    double *t0, double *objfn);
 
+/* Replaces locate_l2_gridSearch__float64 (locate.c:1079-1203): the fp32
+ * variant, same arguments, checks and arithmetic order; host arrays. */
+int locate_l2_gridSearch__float64(int ldgrd, int ngrd, int nobs, int iwantOT, float t0use,
+                                  const int *mask, const float *tobs, const float *tcorr,
+                                  const float *varobs, const float *test, float *t0, float *objfn);
+
+/* ---- relocation grid search over many events (device memory) ---------- */
+/* For every event e and grid point g: the locate.c L2 objective with the
+ * analytic origin time (fp32, locate_l2_gridSearch__float64 arithmetic) of
+ * event e's observations against shared travel-time tables.  Observations
+ * are compacted per event (masked ones removed, reference order): event e
+ * owns [ev_ptr[e], ev_ptr[e+1]); obs_row[j] is the row of `tables` (e.g. the
+ * station), tc[j] = tobs - tcorr, wt[j] = 1/var, xnorm[e] = sum of wt in
+ * order.  out[e*ldgrd + g] = objfn, or -objfn (log joint PDF up to a
+ * constant) when log_pdf != 0; t0 (may be NULL) the same layout. */
+typedef struct mceik_relocate_batch {
+    int ldgrd, ngrd, nev, iwantOT;
+    float t0use;
+    const float *tables;        /* device [nrows][ldgrd]                     */
+    const int *ev_ptr;          /* device [nev+1]                            */
+    const int *obs_row;         /* device [ev_ptr[nev]]                      */
+    const float *tc, *wt;       /* device [ev_ptr[nev]]                      */
+    const float *xnorm;         /* device [nev]                              */
+    float *t0;                  /* device [nev][ldgrd] or NULL               */
+    float *out;                 /* device [nev][ldgrd]                       */
+    int log_pdf;
+} mceik_relocate_batch;
+int mceik_relocate(const mceik_relocate_batch *b, void *stream);
+
 /* ---- batched solves on device memory ---------------------------------- */
 typedef struct mceik_fsm_batch {
     int nx, ny, nz;             /* grid nodes, dx = dy = dz = h              */

@@ -26,6 +26,14 @@ class FsmBatch(C.Structure):
                 ("visit_stats", C.c_void_p)]
 
 
+class RelocateBatch(C.Structure):
+    """mceik_relocate_batch (include/mceik_eikonal.h)."""
+    _fields_ = [("ldgrd", C.c_int), ("ngrd", C.c_int), ("nev", C.c_int), ("iwantOT", C.c_int),
+                ("t0use", C.c_float), ("tables", C.c_void_p), ("ev_ptr", C.c_void_p), ("obs_row", C.c_void_p),
+                ("tc", C.c_void_p), ("wt", C.c_void_p), ("xnorm", C.c_void_p), ("t0", C.c_void_p),
+                ("out", C.c_void_p), ("log_pdf", C.c_int)]
+
+
 class McmcParms(C.Structure):
     _fields_ = [("resdir", C.c_char * 512), ("nburnIn", C.c_int), ("niter", C.c_int), ("keepK", C.c_int)]
 
@@ -68,6 +76,7 @@ class McmcOpts(C.Structure):
 
 # every extern "C" symbol include/*.h declares
 EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "locate_l2_gridSearch__double64",
+           "locate_l2_gridSearch__float64", "mceik_relocate",
            "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
@@ -98,6 +107,10 @@ def lib():
     L.mceik_fsm_batch_solve.argtypes = [C.POINTER(FsmBatch), C.c_void_p, C.c_size_t, C.c_void_p]
     L.mceik_memcpy.restype = C.c_int
     L.mceik_memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    L.locate_l2_gridSearch__float64.restype = C.c_int
+    L.locate_l2_gridSearch__float64.argtypes = [C.c_int] * 4 + [C.c_float] + [C.c_void_p] * 7
+    L.mceik_relocate.restype = C.c_int
+    L.mceik_relocate.argtypes = [C.POINTER(RelocateBatch), C.c_void_p]
     L.mceik_mcmc_init.restype = C.c_int
     L.mceik_mcmc_init.argtypes = [C.POINTER(MceikParms), C.POINTER(StationsStruct), C.POINTER(CatalogStruct),
                                   C.POINTER(McmcOpts), C.c_void_p, C.POINTER(C.c_void_p)]

@@ -26,6 +26,9 @@ hipError_t fsm_to_brick_f32(const float *src, float *dst, const FsmLaunch &L, in
 hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st);
 hipError_t mcmc_init_loglik(const McmcDev &D, hipStream_t st);
 hipError_t mcmc_accept(const McmcDev &D, int keep_slot, hipStream_t st);
+hipError_t l2_gridsearch_f32(int ldgrd, int ngrd, int nev, int iwantOT, float t0use, const int *ev_ptr,
+                             const int *obs_row, const float *tc, const float *wt, const float *xnorm,
+                             const float *test, float *t0, float *objfn, int negate, hipStream_t st);
 hipError_t l2_gridsearch(int ldgrd, int ngrd, int nuse, int iwantOT, double t0use, const int *use,
                          const double *tc, const double *wt, double xnorm, const double *test,
                          double *t0, double *objfn, hipStream_t st);
@@ -383,6 +386,84 @@ out:
     hipFree(d_use); hipFree(d_tc); hipFree(d_wt); hipFree(d_test); hipFree(d_t0); hipFree(d_obj);
     if (rc) printf("%s: device failure\n", fcnm);
     return rc;
+}
+
+// ---------------------------------------------------------------------------
+// locate_l2_gridSearch__float64 drop-in (locate.c:1079-1203): fp32 arithmetic.
+extern "C" int locate_l2_gridSearch__float64(int ldgrd, int ngrd, int nobs, int iwantOT, float t0use,
+                                             const int *mask, const float *tobs, const float *tcorr,
+                                             const float *varobs, const float *test, float *t0, float *objfn)
+{
+    const char *fcnm = "locate_l2_gridSearch__float64";
+    if ((sizeof(float) * (size_t)ldgrd) % 64 != 0 || ldgrd < ngrd || nobs < 1 || !mask || !tobs ||
+        !varobs || !test || !t0 || !objfn) {
+        if ((sizeof(float) * (size_t)ldgrd) % 64 != 0) printf("%s: Error ldgrd must be divisible by 64\n", fcnm);
+        if (ldgrd < ngrd) printf("%s: Error ldgrd < ngrd\n", fcnm);
+        if (!mask) printf("%s: mask is null\n", fcnm);
+        if (!tobs) printf("%s: tobs is null\n", fcnm);
+        if (!varobs) printf("%s: varobs is null\n", fcnm);
+        if (!test) printf("%s: test is null\n", fcnm);
+        if (!t0) printf("%s: t0 is null\n", fcnm);
+        if (!objfn) printf("%s: objfn is null\n", fcnm);
+        return 1;
+    }
+    if (((uintptr_t)t0 % 64) || ((uintptr_t)test % 64) || ((uintptr_t)objfn % 64)) {
+        printf("%s: Input arrays are not 64 bit aligned\n", fcnm);
+        return 1;
+    }
+    std::vector<int> row;
+    std::vector<float> tc, wt;
+    float xnorm = 0.0f;
+    for (int i = 0; i < nobs; i++) {
+        if (mask[i] != 0) continue;
+        tc.push_back(tcorr ? tobs[i] - tcorr[i] : tobs[i]);
+        row.push_back(i);
+        wt.push_back(1.0f / varobs[i]);
+        xnorm = xnorm + wt.back();
+    }
+    const int nuse = (int)row.size();
+    const int ptr[2] = {0, nuse};
+    int *d_row = nullptr, *d_ptr = nullptr;
+    float *d_tc = nullptr, *d_wt = nullptr, *d_xn = nullptr, *d_test = nullptr, *d_t0 = nullptr, *d_obj = nullptr;
+    int rc = 1;
+    const size_t tb = (size_t)ldgrd * nobs * 4, gb = (size_t)ldgrd * 4;
+    if (hipMalloc(&d_row, (nuse + 1) * 4) != hipSuccess || hipMalloc(&d_ptr, 8) != hipSuccess ||
+        hipMalloc(&d_tc, (nuse + 1) * 4) != hipSuccess || hipMalloc(&d_wt, (nuse + 1) * 4) != hipSuccess ||
+        hipMalloc(&d_xn, 4) != hipSuccess || hipMalloc(&d_test, tb) != hipSuccess ||
+        hipMalloc(&d_t0, gb) != hipSuccess || hipMalloc(&d_obj, gb) != hipSuccess)
+        goto out;
+    if (nuse) {
+        hipMemcpy(d_row, row.data(), nuse * 4, hipMemcpyHostToDevice);
+        hipMemcpy(d_tc, tc.data(), nuse * 4, hipMemcpyHostToDevice);
+        hipMemcpy(d_wt, wt.data(), nuse * 4, hipMemcpyHostToDevice);
+    }
+    hipMemcpy(d_ptr, ptr, 8, hipMemcpyHostToDevice);
+    hipMemcpy(d_xn, &xnorm, 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_test, test, tb, hipMemcpyHostToDevice);
+    if (l2_gridsearch_f32(ldgrd, ngrd, 1, iwantOT, t0use, d_ptr, d_row, d_tc, d_wt, d_xn, d_test, d_t0, d_obj, 0,
+                          nullptr) != hipSuccess)
+        goto out;
+    if (hipMemcpy(t0, d_t0, (size_t)ngrd * 4, hipMemcpyDeviceToHost) != hipSuccess) goto out;
+    if (hipMemcpy(objfn, d_obj, (size_t)ngrd * 4, hipMemcpyDeviceToHost) != hipSuccess) goto out;
+    rc = 0;
+out:
+    hipFree(d_row); hipFree(d_ptr); hipFree(d_tc); hipFree(d_wt); hipFree(d_xn);
+    hipFree(d_test); hipFree(d_t0); hipFree(d_obj);
+    if (rc) printf("%s: device failure\n", fcnm);
+    return rc;
+}
+
+// Relocation grid search of many events against one model's station tables
+// (SURVEY s.8f row 2): device arrays, one launch, enqueued on `stream`.
+extern "C" int mceik_relocate(const mceik_relocate_batch *b, void *stream)
+{
+    if (!b || b->ngrd < 1 || b->ldgrd < b->ngrd || b->nev < 1 || !b->tables || !b->ev_ptr || !b->obs_row ||
+        !b->tc || !b->wt || !b->xnorm || !b->out) {
+        fprintf(stderr, "mceik_relocate: invalid batch description\n");
+        return 1;
+    }
+    return l2_gridsearch_f32(b->ldgrd, b->ngrd, b->nev, b->iwantOT, b->t0use, b->ev_ptr, b->obs_row, b->tc, b->wt,
+                             b->xnorm, b->tables, b->t0, b->out, b->log_pdf ? 1 : 0, (hipStream_t)stream) != hipSuccess;
 }
 
 // ---------------------------------------------------------------------------

@@ -160,6 +160,41 @@ __global__ void l2_gridsearch_kernel(int ldgrd, int ngrd, int nuse, int iwantOT,
     }
 }
 
+// fp32 twin of the above (locate.c:1079-1203, locate_l2_gridSearch__float64),
+// batched over events that share travel-time tables: event e uses
+// observations [ev_ptr[e], ev_ptr[e+1]) of the compacted arrays (mask already
+// applied, reference order), row obs_row[j] of `test` (leading dimension
+// ldgrd), tc = tobs - tcorr, wt = 1/var, xnorm[e] = sum wt (host, in order).
+// grid (ceil(ngrd/256), nev): thread = (grid point, event).
+__global__ void l2_gridsearch_f32_kernel(int ldgrd, int ngrd, int iwantOT, float t0use, const int *ev_ptr,
+                                         const int *obs_row, const float *tc, const float *wt, const float *xnorm,
+                                         const float *test, float *t0, float *objfn, int negate)
+{
+    const float sqrt2i = 0.7071067811865475f;
+    const int e = blockIdx.y;
+    const int j0 = ev_ptr[e], j1 = ev_ptr[e + 1];
+    const float xn = xnorm[e];
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < ngrd; g += gridDim.x * blockDim.x) {
+        float t = 0.0f;
+        if (iwantOT == 1) {
+            for (int j = j0; j < j1; j++) {
+                const float w = wt[j] / xn;
+                t = t + w * (tc[j] - test[(size_t)ldgrd * obs_row[j] + g]);
+            }
+        } else {
+            t = t0use;
+        }
+        float o = 0.0f;
+        for (int j = j0; j < j1; j++) {
+            const float w = wt[j] * sqrt2i;
+            const float res = w * (tc[j] - (test[(size_t)ldgrd * obs_row[j] + g] + t));
+            o = o + res * res;
+        }
+        if (t0) t0[(size_t)e * ldgrd + g] = t;
+        objfn[(size_t)e * ldgrd + g] = negate ? -o : o;
+    }
+}
+
 }  // namespace
 
 hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st)
@@ -190,5 +225,16 @@ hipError_t l2_gridsearch(int ldgrd, int ngrd, int nuse, int iwantOT, double t0us
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(l2_gridsearch_kernel, dim3(blocks), dim3(256), 0, st, ldgrd, ngrd, nuse, iwantOT,
                        t0use, use, tc, wt, xnorm, test, t0, objfn);
+    return hipGetLastError();
+}
+
+hipError_t l2_gridsearch_f32(int ldgrd, int ngrd, int nev, int iwantOT, float t0use, const int *ev_ptr,
+                             const int *obs_row, const float *tc, const float *wt, const float *xnorm,
+                             const float *test, float *t0, float *objfn, int negate, hipStream_t st)
+{
+    int bx = (ngrd + 255) / 256;
+    if (bx > 2048) bx = 2048;
+    hipLaunchKernelGGL(l2_gridsearch_f32_kernel, dim3(bx, nev), dim3(256), 0, st, ldgrd, ngrd, iwantOT, t0use,
+                       ev_ptr, obs_row, tc, wt, xnorm, test, t0, objfn, negate);
     return hipGetLastError();
 }

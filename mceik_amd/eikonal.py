@@ -63,6 +63,69 @@ def locate_l2_gridsearch(ldgrd, ngrd, nobs, iwantOT, t0use, mask, tobs, tcorr, v
                                             objfn.ctypes.data_as(C.c_void_p))
 
 
+def locate_l2_gridsearch_f32(ldgrd, ngrd, nobs, iwantOT, t0use, mask, tobs, tcorr, varobs, test, t0, objfn):
+    """locate_l2_gridSearch__float64 (locate.c:1079-1203, the fp32 variant) on the
+    GPU; returns ierr.  test/t0/objfn: 64-byte aligned float32 arrays."""
+    L = _lib.lib()
+    m = np.ascontiguousarray(mask, dtype=np.int32)
+    f = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.float32)
+    to, va, tc = f(tobs), f(varobs), f(tcorr)
+    p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+    return L.locate_l2_gridSearch__float64(int(ldgrd), int(ngrd), int(nobs), int(iwantOT), float(t0use),
+                                           p(m), p(to), p(tc), p(va), p(test), p(t0), p(objfn))
+
+
+def relocate(tables, events, ldgrd=None, iwantOT=1, t0use=0.0, log_pdf=True, stream=0):
+    """Relocation grid search (SURVEY s.8f row 2) of many events against one
+    model's travel-time tables, one GPU launch (mceik_relocate).
+
+    tables : torch float32 CUDA tensor [nrows, ldgrd] (row r = station r's
+             travel times at every grid node, x fastest)
+    events : list of dicts with 'rows' (int table row of each observation),
+             'tobs', 'varobs', optional 'tcorr' and 'mask' (1 = masked),
+             in the reference's observation order
+    returns (out, t0): torch float32 [nev, ldgrd]; out = -objfn if log_pdf
+    else objfn (locate.c L2 with the analytic origin time, fp32).
+    """
+    import torch
+    L = _lib.lib()
+    dev = tables.device
+    nrows, ld = tables.shape
+    ld = ldgrd or ld
+    ptr, rows, tc, wt, xn = [0], [], [], [], []
+    for ev in events:
+        m = np.zeros(len(ev["rows"]), np.int32) if ev.get("mask") is None else np.asarray(ev["mask"])
+        tcorr = ev.get("tcorr")
+        x = np.float32(0.0)
+        for i, r in enumerate(ev["rows"]):
+            if m[i] != 0:
+                continue
+            to = np.float32(ev["tobs"][i])
+            tc.append(to - np.float32(tcorr[i]) if tcorr is not None else to)
+            rows.append(int(r))
+            w = np.float32(1.0) / np.float32(ev["varobs"][i])
+            wt.append(w)
+            x = np.float32(x + w)
+        xn.append(x)
+        ptr.append(len(rows))
+    nev = len(events)
+    t = lambda a, dt: torch.tensor(np.asarray(a, dtype=dt), device=dev)
+    d_ptr, d_rows = t(ptr, np.int32), t(rows if rows else [0], np.int32)
+    d_tc, d_wt, d_xn = t(tc if tc else [0], np.float32), t(wt if wt else [0], np.float32), t(xn, np.float32)
+    out = torch.empty((nev, ld), dtype=torch.float32, device=dev)
+    t0 = torch.empty((nev, ld), dtype=torch.float32, device=dev)
+    b = _lib.RelocateBatch()
+    b.ldgrd, b.ngrd, b.nev, b.iwantOT, b.t0use = ld, int(tables.shape[1]) if ldgrd is None else int(ldgrd), nev, \
+        int(iwantOT), float(t0use)
+    b.ngrd = min(b.ngrd, ld)
+    b.tables, b.ev_ptr, b.obs_row = tables.data_ptr(), d_ptr.data_ptr(), d_rows.data_ptr()
+    b.tc, b.wt, b.xnorm = d_tc.data_ptr(), d_wt.data_ptr(), d_xn.data_ptr()
+    b.t0, b.out, b.log_pdf = t0.data_ptr(), out.data_ptr(), 1 if log_pdf else 0
+    if L.mceik_relocate(C.byref(b), C.c_void_p(stream)) != 0:
+        raise RuntimeError("mceik_relocate failed")
+    return out, t0
+
+
 def aligned_empty(n, dtype=np.float64, align=64):
     """numpy array whose data pointer is `align`-byte aligned (locate.c:967-974 requirement)."""
     itemsize = np.dtype(dtype).itemsize

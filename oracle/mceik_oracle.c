@@ -165,6 +165,51 @@ int oracle_locate_l2_gridsearch_f64(int ldgrd, int ngrd, int nobs, int iwantOT, 
     return 0;
 }
 
+/* locate_l2_gridSearch__float64 (locate.c:1079-1203): the same loops in fp32
+ * (the reference's float accumulations, 1.0f/var, sqrt2i as a float). */
+int oracle_locate_l2_gridsearch_f32(int ldgrd, int ngrd, int nobs, int iwantOT, float t0use,
+                                    const int *mask, const float *tobs, const float *tcorr,
+                                    const float *varobs, const float *test,
+                                    float *t0, float *objfn)
+{
+    if (ldgrd < ngrd || nobs < 1 || !mask || !tobs || !varobs || !test || !t0 || !objfn)
+        return 1;
+    for (int g = 0; g < ngrd; g++) objfn[g] = 0.0f;
+    int *use = (int *)malloc(sizeof(int) * nobs);
+    float *tc = (float *)malloc(sizeof(float) * nobs), *wt = (float *)malloc(sizeof(float) * nobs);
+    int nuse = 0;
+    float xnorm = 0.0f;
+    for (int i = 0; i < nobs; i++) {
+        if (mask[i] != 0) continue;
+        tc[nuse] = tcorr ? tobs[i] - tcorr[i] : tobs[i];
+        use[nuse] = i;
+        wt[nuse] = 1.0f / varobs[i];
+        xnorm = xnorm + wt[nuse];
+        nuse++;
+    }
+    if (iwantOT == 1) {
+        for (int g = 0; g < ngrd; g++) t0[g] = 0.0f;
+        for (int j = 0; j < nuse; j++) {
+            float w = wt[j] / xnorm, to = tc[j];
+            const float *te = test + (size_t)ldgrd * use[j];
+            for (int g = 0; g < ngrd; g++) t0[g] = t0[g] + w * (to - te[g]);
+        }
+    } else {
+        for (int g = 0; g < ngrd; g++) t0[g] = t0use;
+    }
+    const float sqrt2i = 0.7071067811865475f;
+    for (int j = 0; j < nuse; j++) {
+        float w = wt[j] * sqrt2i, to = tc[j];
+        const float *te = test + (size_t)ldgrd * use[j];
+        for (int g = 0; g < ngrd; g++) {
+            float res = w * (to - (te[g] + t0[g]));
+            objfn[g] = objfn[g] + res * res;
+        }
+    }
+    free(use); free(tc); free(wt);
+    return 0;
+}
+
 /* Fortran variant (gridsearch.f90:382-456): t0 weight 1/(var_i * sum var),
  * logPDF weight sqrt(1/2)/var_i.  Returns the 0-based argmin (MINLOC). */
 int oracle_gridsearch_f90_f64(int ldgrd, int ngrd, int nobs, int iwantOT, const int *mask,

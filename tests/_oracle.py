@@ -76,6 +76,18 @@ def locate_l2(ldgrd, ngrd, nobs, iwant, t0use, mask, tobs, tcorr, varobs, test):
     return ierr, t0, obj
 
 
+def locate_l2_f32(ldgrd, ngrd, nobs, iwant, t0use, mask, tobs, tcorr, varobs, test):
+    t0 = np.zeros(ngrd, np.float32); obj = np.zeros(ngrd, np.float32)
+    m = np.ascontiguousarray(mask, dtype=np.int32)
+    f = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.float32)
+    tobs, tcorr, varobs, test = f(tobs), f(tcorr), f(varobs), f(test)
+    L = lib()
+    L.oracle_locate_l2_gridsearch_f32.argtypes = [C.c_int] * 4 + [C.c_float] + [C.c_void_p] * 7
+    ierr = L.oracle_locate_l2_gridsearch_f32(ldgrd, ngrd, nobs, iwant, t0use, _p(m), _p(tobs), _p(tcorr),
+                                             _p(varobs), _p(test), _p(t0), _p(obj))
+    return ierr, t0, obj
+
+
 def gridsearch_f90(ldgrd, ngrd, nobs, iwant, mask, tobs, varobs, test):
     logpdf = np.zeros(ngrd); t0 = C.c_double(0)
     m = np.ascontiguousarray(mask, dtype=np.int32)

@@ -177,6 +177,24 @@ def make_locate():
         print(f"locate_l2 {tag}: argmin={int(np.argmin(obj))} true={4*nx*ny+9*nx+12}")
     np.savez_compressed(os.path.join(HERE, "locate_l2.npz"), **out)
 
+    # the fp32 variant (locate.c:1079-1203) on the same inputs cast to float32
+    g = lib.locate_l2_gridSearch__float64
+    g.restype = C.c_int
+    g.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_float] + [C.c_void_p] * 7
+    test32 = aligned(nobs * ldgrd, np.float32)
+    test32[:] = np.asarray(test, dtype=np.float32)
+    tobs32, varobs32, tcorr32 = (np.asarray(a, dtype=np.float32) for a in (tobs, varobs, tcorr))
+    o32 = dict(ldgrd=ldgrd, ngrd=ngrd, nobs=nobs, tobs=tobs32, varobs=varobs32, tcorr=tcorr32, mask=mask,
+               test=np.array(test32))
+    for tag, iwant, t0use, use_tc, m in (("ot", 1, 0.0, True, mask), ("fixed", 0, 4.0, False, np.zeros_like(mask))):
+        t0 = aligned(ngrd, np.float32); obj = aligned(ngrd, np.float32)
+        ierr = g(ldgrd, ngrd, nobs, iwant, t0use, _ptr(m), _ptr(tobs32), _ptr(tcorr32) if use_tc else None,
+                 _ptr(varobs32), _ptr(test32), _ptr(t0), _ptr(obj))
+        assert ierr == 0
+        o32[f"{tag}_t0"] = np.array(t0); o32[f"{tag}_objfn"] = np.array(obj)
+        print(f"locate_l2 f32 {tag}: argmin={int(np.argmin(obj))}")
+    np.savez_compressed(os.path.join(HERE, "locate_l2_f32.npz"), **o32)
+
 
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF, "libfsm3d_ref.so")):

@@ -219,3 +219,50 @@ def test_locate_l2_gpu_bitwise_vs_reference():
     assert np.array_equal(obj.view(np.uint64), g["fixed_objfn"].view(np.uint64))
     # reference error behaviour: ldgrd*8 % 64 != 0
     assert locate_l2_gridsearch(ld + 1, ng, no, 1, 0.0, g["mask"], g["tobs"], None, g["varobs"], test, t0, obj) == 1
+
+
+def test_locate_l2_f32_gpu_bitwise_vs_reference():
+    """locate_l2_gridSearch__float64 drop-in vs the compiled reference (golden)."""
+    from mceik_amd.eikonal import aligned_empty, locate_l2_gridsearch_f32
+    _dev()
+    g = dict(np.load(os.path.join(GOLD, "locate_l2_f32.npz"), allow_pickle=False))
+    ld, ng, no = int(g["ldgrd"]), int(g["ngrd"]), int(g["nobs"])
+    test = aligned_empty(g["test"].size, np.float32); test[:] = g["test"]
+    t0 = aligned_empty(ng, np.float32); obj = aligned_empty(ng, np.float32)
+    assert locate_l2_gridsearch_f32(ld, ng, no, 1, 0.0, g["mask"], g["tobs"], g["tcorr"], g["varobs"],
+                                    test, t0, obj) == 0
+    assert np.array_equal(t0.view(np.uint32), g["ot_t0"].view(np.uint32))
+    assert np.array_equal(obj.view(np.uint32), g["ot_objfn"].view(np.uint32))
+    assert locate_l2_gridsearch_f32(ld, ng, no, 0, 4.0, np.zeros(no), g["tobs"], None, g["varobs"],
+                                    test, t0, obj) == 0
+    assert np.array_equal(obj.view(np.uint32), g["fixed_objfn"].view(np.uint32))
+    # the reference's checks: ldgrd*4 % 64 != 0 -> ierr 1
+    assert locate_l2_gridsearch_f32(ld + 1, ng, no, 1, 0.0, g["mask"], g["tobs"], None, g["varobs"],
+                                    test, t0, obj) == 1
+
+
+def test_relocate_batch_matches_reference_per_event():
+    """Batched relocation (all events against shared tables, one launch) equals
+    the reference fp32 L2 grid search event by event (oracle restatement,
+    itself pinned to locate.c by the golden test)."""
+    from mceik_amd.eikonal import relocate
+    dev = _dev()
+    g = dict(np.load(os.path.join(GOLD, "locate_l2_f32.npz"), allow_pickle=False))
+    ld, ng, no = int(g["ldgrd"]), int(g["ngrd"]), int(g["nobs"])
+    tables = torch.tensor(g["test"].reshape(no, ld), device=dev)
+    rng = np.random.default_rng(11)
+    events = []
+    for e in range(5):
+        rows = rng.permutation(no)[: 6 + e]
+        mask = (rng.random(rows.size) < 0.2).astype(np.int32)
+        events.append(dict(rows=rows, tobs=g["tobs"][rows] + np.float32(0.3 * e), varobs=g["varobs"][rows],
+                           tcorr=g["tcorr"][rows], mask=mask))
+    out, t0 = relocate(tables, events, log_pdf=True)
+    out = out.cpu().numpy(); t0 = t0.cpu().numpy()
+    for e, ev in enumerate(events):
+        sub_test = g["test"].reshape(no, ld)[ev["rows"]].ravel()
+        ierr, rt0, robj = O.locate_l2_f32(ld, ng, len(ev["rows"]), 1, 0.0, ev["mask"], ev["tobs"], ev["tcorr"],
+                                          ev["varobs"], sub_test)
+        assert ierr == 0
+        assert np.array_equal(t0[e, :ng].view(np.uint32), rt0.view(np.uint32))
+        assert np.array_equal((-out[e, :ng]).view(np.uint32), robj.view(np.uint32))

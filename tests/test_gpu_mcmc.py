@@ -105,3 +105,41 @@ def test_kept_samples():
     for k, (v, lg) in enumerate(states):
         assert np.array_equal(kv[k], v)
         assert np.array_equal(kl[k], lg)
+
+
+def test_posterior_h5io_files(tmp_path):
+    """Kept samples -> the reference's HDF5 posterior (h5io.c layout): the
+    stored P tables are the GPU forward of each kept model bitwise (fp32
+    twin), and each event's logJPDF is the relocation grid search over those
+    tables; noise-free picks of the true model put its maximum on the event
+    node."""
+    _dev()
+    from mceik_amd import h5io, mcmc
+    p = _problem(n=20, nstat=4, nev=3)
+    s = mcmc.Sampler(p, nchains=2, chain_offset=0, max_samples=2)
+    s.run(2)
+    kept, _ = s.samples()
+    s.close()
+    models = np.concatenate([kept.reshape(-1, p.ncell)[:2], p.v_true[None]], 0)
+    tt_true = mcmc.picks_from_forward(0, precision=32)(p)          # [nstat, nev] at the event nodes
+    p.tobs = np.array([tt_true[p.obs_stat[k], e] for e in range(p.nevents)
+                       for k in range(p.obs_ptr[e], p.obs_ptr[e + 1])], dtype=np.float64)
+    ttn, locn = h5io.write_posterior(p, models, str(tmp_path), "post")
+    assert ttn.endswith("post_ttimes.h5") and locn.endswith("post_locations.h5")
+    k, j, i = np.meshgrid(np.arange(p.nz), np.arange(p.ny), np.arange(p.nx), indexing="ij")
+    cell = ((k // p.nrz) * p.ncy + j // p.nry) * p.ncx + i // p.nrx
+    with h5io.H5File.open(ttn) as f:
+        assert f.dims() == (p.nx, p.ny, p.nz)
+        for m in range(models.shape[0]):
+            slow = (1.0 / models[m].astype(np.float32)).astype(np.float32)
+            for st in range(p.nstat):
+                got = f.read_ttimes(st + 1, m + 1)
+                ref, _, _ = O.eikonal_solve(p.nx, p.ny, p.nz, slow[cell].ravel(), p.h,
+                                            np.array([[0.0, p.sx[st], p.sy[st], p.sz[st]]]), maxit=p.maxit,
+                                            tol=p.tol, dtype=np.float32)
+                assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (m, st)
+    with h5io.H5File.open(locn) as f:
+        for e in range(p.nevents):
+            lp = f.read_logjpdf(models.shape[0], e + 1)                # the true model
+            assert int(np.argmax(lp)) == int(p.ev_node[e])
+            assert lp.max() <= 0.0
