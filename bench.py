@@ -110,7 +110,8 @@ def main():
     from mceik_amd import mcmc
 
     cfg = mcmc.CONFIGS[args.config]
-    per_gpu = args.chains or (cfg["nchains"] if args.config != "C4" else cfg["nchains"] // 8)
+    # C4 / C5 are quoted for 8 GPUs: their chain counts are totals
+    per_gpu = args.chains or (cfg["nchains"] // 8 if args.config in ("C4", "C5") else cfg["nchains"])
     # problem geometry and start models are pure numpy: the CPU baseline runs
     # before anything touches the GPU (its workers are spawned processes)
     p = mcmc.make_problem(args.config, picks="analytic")

@@ -112,6 +112,25 @@ static int device_cus()
     return g_device_cus;
 }
 
+// Scratch budget for the per-wave u / u0 fields, fixed at the first call (so
+// workspace_bytes and batch_solve agree): MCEIK_FSM_WS_GB if set, else half of
+// the device's total memory (144 GB on a 288-GB MI355X).
+static size_t ws_budget_bytes()
+{
+    static size_t budget = 0;
+    if (budget == 0) {
+        const char *e = getenv("MCEIK_FSM_WS_GB");
+        double gb = e ? atof(e) : 0.0;
+        if (gb > 0.0) {
+            budget = (size_t)(gb * 1073741824.0);
+        } else {
+            size_t fr = 0, tot = 0;
+            budget = hipMemGetInfo(&fr, &tot) == hipSuccess && tot ? tot / 2 : (size_t)96 << 30;
+        }
+    }
+    return budget;
+}
+
 // Waves a launch keeps resident (one solve each): occupancy x CUs, at most nsolve.
 static int batch_waves(const FsmLaunch &L, int is_double)
 {
@@ -136,6 +155,15 @@ static WsLayout ws_layout(const mceik_fsm_batch *b)
     size_t es = is_double ? 8 : 4;
     WsLayout w;
     w.nwaves = batch_waves(L, is_double);
+    // Every resident wave owns a u and a u0 scratch field: cap the waves so the
+    // scratch stays within a fixed budget (deterministic across calls; 256^3
+    // fp32 fields are 67 MB, 2048 waves would need 275 GB).  Waves then take
+    // several solves each from the queue.
+    {
+        const size_t per_wave = 2 * L.field_elems * es;
+        const long cap = (long)(ws_budget_bytes() / (per_wave ? per_wave : 1));
+        if (cap >= 1 && w.nwaves > cap) w.nwaves = (int)cap;
+    }
     w.counter = 0;
     w.slow = 1024;
     size_t slow_bytes = b->slow_mode == 0 ? (size_t)b->nmodel * L.field_elems * es : 0;

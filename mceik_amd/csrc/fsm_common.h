@@ -64,7 +64,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[4] = o; o += mceik_align16(nt * 4);
     off[5] = o; o += mceik_align16(nt * 2);
     off[6] = o;                                   // (unused)
-    off[7] = o; o += 16;
+    off[7] = o; o += 32;                          // ring[4] + debug[4]
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 128 * es;
     off[10] = o; o += 128 * es;

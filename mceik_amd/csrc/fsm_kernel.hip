@@ -572,6 +572,12 @@ __device__ __forceinline__ void admit_tile(const FsmLaunch &L, const Smem<R> &S,
     const u4v ci = column_info<R>(L, bc, entry, pos, u0flag, lx, ly, lxs, lys, rx, ry);
     asm volatile("" ::: "memory");
     S.cinfo[(pos & 3) * 64 + threadIdx.x] = ci;
+#ifdef MCEIK_BLOCK_STATS
+    if (threadIdx.x == 0 && L.visit_stats) {
+        atomicAdd(L.visit_stats + 2, (unsigned long long)__builtin_popcount(((unsigned *)S.ring)[4 + (pos & 3)]));
+        ((unsigned *)S.ring)[4 + (pos & 3)] = 0;
+    }
+#endif
     if (threadIdx.x == 0) {
         S.u0ep[id] = (unsigned short)(it + 1);
         S.lastproc[id] = clock;
@@ -853,7 +859,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         notconv |= nc && val;
         if (L.visit_stats) {                                // wave-uniform; SALU popcounts
             segs += __builtin_popcountll(__ballot(val && (b0.fl & C_ACT)));
+#ifdef MCEIK_BLOCK_STATS
+            // debug: changed 4-brick z blocks per tile visit (ring slot sp & 3)
+            if (changed) atomicOr((unsigned *)(S.ring + 4 + (b0.sp & 3)), 1u << (b0.zb8 >> 5));
+#else
             segs_changed += __builtin_popcountll(__ballot(changed));
+#endif
         }
 
         // ---- write-back, u0 at a tile's first visit of the iteration, change stamps
