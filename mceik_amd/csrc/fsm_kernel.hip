@@ -606,33 +606,40 @@ __device__ __forceinline__ double fmin_(double a, double b) { return __builtin_f
 
 // Godunov update without the error code (fast path): fp32 values identical to
 // godunov_bl (a1 == UN or an overflowing / NaN candidate gives UN either way).
+// ff = f*f and ff2 = ff + ff come from the caller (once per slowness cell).
 template <bool FAST>
-__device__ __forceinline__ float godunov_v(float a, float b, float c, float f)
+__device__ __forceinline__ float godunov_v(float a, float b, float c, float f, float ff, float ff2)
 {
-    // sort by bit pattern (non-negative, non-NaN inputs; see fmin_)
+    // sort by bit pattern (non-negative, non-NaN inputs; see fmin_): v_min3 / v_max3 / v_med3
     const unsigned ia = __builtin_bit_cast(unsigned, a), ib = __builtin_bit_cast(unsigned, b),
                    ic = __builtin_bit_cast(unsigned, c);
-    const unsigned lo = __builtin_elementwise_min(ia, ib), hi = __builtin_elementwise_max(ia, ib);
-    const float a1 = __builtin_bit_cast(float, __builtin_elementwise_min(lo, ic));
-    const float a3 = __builtin_bit_cast(float, __builtin_elementwise_max(hi, ic));
-    const float a2 = __builtin_bit_cast(float, __builtin_elementwise_max(lo, __builtin_elementwise_min(hi, ic)));
+    unsigned u1, u2, u3;
+    // (written as asm: the instruction selector shares min(a,b) / max(a,b)
+    // between the three and emits five ops)
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(u1) : "v"(ia), "v"(ib), "v"(ic));
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(u2) : "v"(ia), "v"(ib), "v"(ic));
+    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(u3) : "v"(ia), "v"(ib), "v"(ic));
+    const float a1 = __builtin_bit_cast(float, u1), a2 = __builtin_bit_cast(float, u2),
+                a3 = __builtin_bit_cast(float, u3);
     const float d2 = a2 - a1, d3 = a3 - a1;
-    const float ff = f * f, e = d3 - d2;
+    const float e = d3 - d2;
     const float d22 = d2 * d2, d33 = d3 * d3;
     const bool two = (d33 + e * e) >= ff;
-    const float r2 = (ff + ff) - d22;
+    const float r2 = ff2 - d22;
     const float sm = d2 + d3;
     const float q = (d22 + d33) - ff;
     const float disc = sm * sm - 3.0f * q;
-    const float s = FAST ? sqrt_normal(two ? r2 : disc) : __builtin_sqrtf(two ? r2 : disc);
-    const float y23 = two ? 0.5f * (d2 + s) : (sm + s) * (1.0f / 3.0f);
+    const float rad = two ? r2 : disc;
+    const float s = FAST ? sqrt_normal(rad) : __builtin_sqrtf(rad);
+    // two: 0.5 * (d2 + s); else (sm + s) * (1/3)  (same products, one multiply)
+    const float y23 = ((two ? d2 : sm) + s) * (two ? 0.5f : (1.0f / 3.0f));
     const float y = !(f > d2) ? f : y23;
     // x >= UN, +inf or NaN -> UN: unsigned min with the bits of FLT_MAX (x >= +0)
     const unsigned ix = __builtin_bit_cast(unsigned, a1 + y);
     return __builtin_bit_cast(float, __builtin_elementwise_min(ix, 0x7f7fffffu));
 }
 template <bool FAST>
-__device__ __forceinline__ double godunov_v(double a, double b, double c, double f)
+__device__ __forceinline__ double godunov_v(double a, double b, double c, double f, double, double)
 {
     int e;
     return godunov(a, b, c, f, e);
@@ -641,7 +648,7 @@ __device__ __forceinline__ double godunov_v(double a, double b, double c, double
 // x/y neighbour minima and f = s*h of slot pj.  The x and y neighbours come
 // from the other lanes' r (updated in their previous step) and n, which the
 // current step does not modify, so any slot may gather them at any time.
-template <typename R, int SLOWMODE, int ZSH, bool GENERIC>
+template <typename R, int SLOWMODE, int ZSH, bool GENERIC, bool WANTF>
 __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, const R (&c)[8],
                                           const R (&n)[8], const R (&r)[8], int pj, int aup, int adn,
                                           bool xp, bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
@@ -651,7 +658,8 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
     const R self = c[pj];
     const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
     const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
-    if (SLOWMODE == 2) {
+    if (!WANTF) {
+    } else if (SLOWMODE == 2) {
         if (ZSH >= 0 && !GENERIC) {
             fv = (R)S.cc[b0.ccb + (pj >> (ZSH < 0 ? 0 : ZSH))];
         } else {
@@ -703,6 +711,9 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
     const bool first = (fl & F_FIRST) != 0, last = (fl & F_LAST) != 0;
     int aup = ((lane - 8) & 63) * 4, adn = ((lane + 8) & 63) * 4;
     asm volatile("" : "+v"(aup), "+v"(adn));
+    // fast fp32 path over the LDS cell cache: f, f*f, 2f*f per cell
+    constexpr bool CELLF = SLOWMODE == 2 && ZSH >= 0 && !GENERIC && sizeof(R) == 4;
+    R fc = 0, ffc = 0, ff2c = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const int pj = RZ ? 7 - j : j;
@@ -710,7 +721,16 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
         const int pnext = RZ ? pj - 1 : pj + 1;
         const R self = c[pj];
         R ux, uy, fv;
-        gather_xy<R, SLOWMODE, ZSH, GENERIC>(L, S, b0, c, n, r, pj, aup, adn, xp, xn, yp, yn, ux, uy, fv);
+        gather_xy<R, SLOWMODE, ZSH, GENERIC, !CELLF>(L, S, b0, c, n, r, pj, aup, adn, xp, xn, yp, yn, ux, uy, fv);
+        if (CELLF) {
+            // one LDS read and one f*f per slowness cell (2^ZSH slots)
+            if (j == 0 || (pj >> (ZSH < 0 ? 0 : ZSH)) != (pprev >> (ZSH < 0 ? 0 : ZSH))) {
+                fc = (R)S.cc[b0.ccb + (pj >> (ZSH < 0 ? 0 : ZSH))];
+                ffc = fc * fc;
+                ff2c = ffc + ffc;
+            }
+            fv = fc;
+        }
         R zup, zdn;
         if (GENERIC) {
             const int zabs = b0.zb8 + pj;
@@ -732,7 +752,8 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
             nv = upd ? fmin_(self, ub) : self;
             if ((fl & C_00) && zabs == 0) ierr_last = upd ? e : 0;
         } else {
-            nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv));
+            const R ffv = CELLF ? ffc : fv * fv;
+            nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv, ffv, CELLF ? ff2c : ffv + ffv));
         }
         const bool dec = nv < self;
         nc |= dec && self >= T;
