@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v8"          # bump when the sweep kernel changes; profiles/traffic.json must match
+KERNEL_REV = "fsm-v10"          # bump when the sweep kernel changes; profiles/traffic.json must match
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -161,7 +161,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    fsm_ms, nlaunch, iters, (tiles, segs, segs_changed) = smp.fsm_stats()
+    fsm_ms, nlaunch, iters, (bricks, segs, segs_changed) = smp.fsm_stats()
     _, logl, nacc, _ = smp.state()
     smp.close()
 
@@ -172,10 +172,10 @@ def main():
         b = _lib.FsmBatch(); b.precision = 32; b.slow_mode = 1; b.nstat = p.nstat
         b.nrx, b.nry, b.nrz = p.nref
         bpn = _lib.lib().mceik_fsm_bytes_per_node_sweep(C.byref(b))
-        # algorithmic bytes: every node of every VISITED tile (tiles whose inputs did
-        # not change since their last visit are skipped by the kernel)
-        ntiles = -(-p.nx // 8) * -(-p.ny // 8)
-        alg_bytes = tiles * (n_nodes / ntiles) * bpn      # this rank's launches
+        # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
+        # inputs did not change since their last visit are skipped)
+        nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
+        alg_bytes = bricks * (n_nodes / nbricks) * bpn    # this rank's launches
         full_bytes = iters * 8.0 * n_nodes * bpn          # the same iterations without skipping
         avg_ms = fsm_ms / max(nlaunch, 1)
         achieved = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
@@ -211,7 +211,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
                          "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),
                          "iterations_per_solve": round(iters / max(nlaunch, 1) / (per_gpu * p.nstat), 3),
-                         "tile_visit_fraction": round(tiles / max(1.0, iters * 8.0 * ntiles), 4),
+                         "brick_visit_fraction": round(bricks / max(1.0, iters * 8.0 * nbricks), 4),
                          "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),
                          "full_sweep_equiv_GBs": round(full_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9, 1)},
             "cpu_baseline": cpu,

@@ -52,8 +52,8 @@ int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max
 int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept);
 /* FSM accounting since init (or the last reset): kernel time of every FSM
  * launch from hipEvents on the sampler's stream (ms), launches, and the
- * sum over solves of executed iterations (8 sweeps each) and visits[3] = tile
- * visits (8x8 columns x nz in one sweep; unchanged tiles are skipped), column
+ * sum over solves of executed iterations (8 sweeps each) and visits[3] = brick
+ * visits (8x8x8 nodes in one sweep; unchanged z-blocks are skipped), column
  * segments updated, segments changed (mceik_fsm_batch.visit_stats). Synchronises. */
 int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsigned long long *iters,
                          unsigned long long *visits, int reset);

@@ -92,7 +92,7 @@ typedef struct mceik_fsm_batch {
     unsigned long long *iter_total;  /* device counter += iterations of every solve, or NULL */
     int fast_sqrt;              /* 1: caller guarantees h*slowness >= 1e-12 (cells mode, fp32):
                                    use the shorter correctly rounded sqrt (same results) */
-    unsigned long long *visit_stats; /* device [3] += tile visits (8x8 columns x nz, one sweep; tiles
+    unsigned long long *visit_stats; /* device [3] += brick visits (8x8x8 nodes, one sweep; z-blocks
                                         whose inputs did not change are skipped), column segments
                                         (8 nodes) updated, segments that changed; or NULL */
 } mceik_fsm_batch;

@@ -80,16 +80,23 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.magic_ry = ((1u << 20) + L.nry - 1) / L.nry;
     L.magic_rz = ((1u << 20) + L.nrz - 1) / L.nrz;
     L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab;
-    // LDS cell cache when every tile's cells fit (2 x 2 x ncz at nref = 4)
+    // LDS cell cache when every z-block's cells fit (2 x 2 x 8 at nref = 4, kb = 4)
     {
-        auto span = [](int t, int n, int nr) {
-            int a = t * 8, e = t * 8 + 7 < n - 1 ? t * 8 + 7 : n - 1;
-            return e / nr - a / nr + 1;
-        };
-        int mx = 0, my = 0;
-        for (int t = 0; t < L.ntx; t++) { int v = span(t, L.nx, L.nrx); mx = v > mx ? v : mx; }
-        for (int t = 0; t < L.nty; t++) { int v = span(t, L.ny, L.nry); my = v > my ? v : my; }
-        L.cell_cache = b->slow_mode == 1 && mx * my * L.ncz <= 256 && L.nx < 4096 && L.ny < 4096 && L.nz < 4096;
+        auto span = [](int a, int e, int nr) { return e / nr - a / nr + 1; };
+        int mx = 0, my = 0, mz = 0;
+        for (int t = 0; t < L.ntx; t++) {
+            int v = span(t * 8, t * 8 + 7 < L.nx - 1 ? t * 8 + 7 : L.nx - 1, L.nrx); mx = v > mx ? v : mx;
+        }
+        for (int t = 0; t < L.nty; t++) {
+            int v = span(t * 8, t * 8 + 7 < L.ny - 1 ? t * 8 + 7 : L.ny - 1, L.nry); my = v > my ? v : my;
+        }
+        for (int t = 0; t < L.nzk; t++) {
+            int a = t * L.kb * 8, e = a + L.kb * 8 - 1 < L.nz - 1 ? a + L.kb * 8 - 1 : L.nz - 1;
+            int v = span(a, e, L.nrz); mz = v > mz ? v : mz;
+        }
+        L.ccb = mx * my * mz;
+        L.cell_cache = b->slow_mode == 1 && L.ccb <= MCEIK_CC_MAX && L.nx < 4096 && L.ny < 4096 && L.nz < 4096;
+        if (!L.cell_cache) L.ccb = 0;
     }
     L.fast_sqrt = b->fast_sqrt;
     L.niter = b->niter; L.ierr = b->ierr;
@@ -207,7 +214,8 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
             return 1;
         }
         if (fsm_lds_bytes(G, b->precision == 64 ? 8 : 4) > MCEIK_MAX_LDS) {
-            fprintf(stderr, "mceik_fsm_batch_solve: %d x %d column tiles exceed the LDS tile tables\n", G.ntx, G.nty);
+            fprintf(stderr, "mceik_fsm_batch_solve: %d x %d x %d z-blocks exceed the LDS block tables\n", G.ntx, G.nty,
+                    G.nzk);
             return 1;
         }
     }

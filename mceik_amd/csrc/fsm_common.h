@@ -9,12 +9,17 @@
 #define MCEIK_MAX_SRC 8          // point sources per solve (box BCs, fsm3d.f90:762-840)
 #define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
 #define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
-#define MCEIK_MIN_SB 12          // virtual bricks per tile (>= nzb); halo lags need >= 12
+#define MCEIK_KB 4               // bricks per z-block (stream position) when the block tables fit in LDS
+#define MCEIK_MAX_BLOCKS 1024    // per-block clocks in LDS: at most this many z-blocks per field
 
 // One batched launch: nsolve = nmodel * nstat solves; solve id = model*nstat + station.
 struct FsmLaunch {
     int nx, ny, nz;              // eikonal grid (nodes); dx = dy = dz = h
-    int ntx, nty, nzb, sb, ntiles;
+    int ntx, nty, nzb, ntiles;
+    int kb, nzk, nblocks, nr;    // bricks per z-block (= steps per stream position), z-blocks per column,
+                                 // z-blocks per field, stream ring size (positions in flight)
+    int infl, vis;               // positions a visit stays in flight / min distance to an upwind x/y visit
+    int ccb;                     // cell-cache floats per stream position (SLOWMODE 2)
     int maxit, max_sweeps;       // max_sweeps < 0: unlimited (debug bisection aid)
     double tol, h, x0, y0, z0;
     double conv_thresh;          // T: nodes >= T converge iff unchanged
@@ -44,31 +49,31 @@ struct FsmLaunch {
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 
 // LDS of one solve wave (byte offsets, shared by host and device):
-//  0 BC boxes [MAX_SRC][6] int | 1 cell cache [3][256] float (cached mode) |
-//  2 diagonal tile order int | 3 lastproc int | 4 lastchg int | 5 u0 epoch u16 |
-//  (all [ntiles]) 6 unused | 7 stream ring [4] int |
+//  0 BC boxes [MAX_SRC][6] int | 1 cell cache [nr][ccb] float (cached mode) |
+//  2 diagonal tile order int [ntiles] | 3 lastproc int [nblocks] | 4 lastchg int [nblocks] |
+//  5 u0 epoch u16 [nblocks] | 6 stream entries int [nr] | 7 run scratch int [8] |
 //  8 staged f [8][64] R (uncached) | 9 x halos [8][2][8] R | 10 y halos [8][2][8] R |
-//  11 column info [4][64] uint4
-#define MCEIK_CC_MAX 256
+//  11 column info [nr][64] uint4
+#define MCEIK_CC_MAX 256         // cell-cache floats per position, upper bound
 #define MCEIK_SMEM_ARRAYS 12
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
 static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, size_t es, size_t *off)
 {
     const bool cached = L.slow_mode != 0 && L.cell_cache;
-    const size_t nt = (size_t)L.ntiles;
+    const size_t nt = (size_t)L.ntiles, nb = (size_t)L.nblocks, nr = (size_t)L.nr;
     size_t o = 0;
     off[0] = o; o += mceik_align16(MCEIK_MAX_SRC * 6 * 4);
-    off[1] = o; o += cached ? 3 * MCEIK_CC_MAX * 4 : 0;
+    off[1] = o; o += cached ? mceik_align16(nr * L.ccb * 4) : 0;
     off[2] = o; o += mceik_align16(nt * 4);
-    off[3] = o; o += mceik_align16(nt * 4);
-    off[4] = o; o += mceik_align16(nt * 4);
-    off[5] = o; o += mceik_align16(nt * 2);
-    off[6] = o;                                   // (unused)
-    off[7] = o; o += 32;                          // ring[4] + debug[4]
+    off[3] = o; o += mceik_align16(nb * 4);
+    off[4] = o; o += mceik_align16(nb * 4);
+    off[5] = o; o += mceik_align16(nb * 2);
+    off[6] = o; o += mceik_align16(nr * 4);
+    off[7] = o; o += 32;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 128 * es;
     off[10] = o; o += 128 * es;
-    off[11] = o; o += 4 * 64 * 16;
+    off[11] = o; o += nr * 64 * 16;
     return o;
 }
 static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
@@ -79,15 +84,32 @@ static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
 #define MCEIK_MAX_LDS (64 * 1024)   // dynamic LDS without a launch attribute
 
 // Fills the tile geometry of a launch from nx, ny, nz (es: element bytes).
-// Field layout (DESIGN.md s.3.1): per 8x8 column tile, z-major groups of one
+// Field layout (DESIGN.md s.3.2): per 8x8 column tile, z-major groups of one
 // 128-B line per column (32 fp32 / 16 fp64 z values), columns in colpos order.
+// Stream: positions of kb z-bricks (a z-block); kb = 4 when
+// the per-block tables fit, else the smallest power of two that fits (up to
+// the whole column).  Timing rules of the lane pipeline (lag <= 14 steps,
+// loads issued 2 steps ahead, a store is visible to loads issued >= 3 steps
+// later): a visit stays in flight (its changes unknown) for
+// infl = 1 + ceil(16 / kb) positions; an upwind x/y neighbour visit must be
+// >= vis = ceil(12 / kb) positions back; the ring keeps nr = 2 + ceil(16 / kb)
+// positions (the oldest lane reads its position's column info and cells up
+// to kb + 13 steps after the position starts; one position of margin).
 static inline void fsm_geometry(FsmLaunch *L, int es)
 {
     L->ntx = mceik_div_up(L->nx, MCEIK_TILE);
     L->nty = mceik_div_up(L->ny, MCEIK_TILE);
     L->nzb = mceik_div_up(L->nz, MCEIK_TILE);
-    L->sb = L->nzb > MCEIK_MIN_SB ? L->nzb : MCEIK_MIN_SB;
     L->ntiles = L->ntx * L->nty;
+    int kb = L->nzb < MCEIK_KB ? L->nzb : MCEIK_KB;
+    while (kb < L->nzb && (long)L->ntiles * mceik_div_up(L->nzb, kb) > MCEIK_MAX_BLOCKS) kb *= 2;
+    if (kb > L->nzb) kb = L->nzb;
+    L->kb = kb;
+    L->nzk = mceik_div_up(L->nzb, kb);
+    L->nblocks = L->ntiles * L->nzk;
+    L->infl = 1 + mceik_div_up(16, kb);
+    L->vis = mceik_div_up(12, kb);
+    L->nr = 2 + mceik_div_up(16, kb);
     const int bpl = 16 / es;                     // 8-z bricks per 128-B line
     L->nzq = mceik_div_up(L->nzb, bpl);
     L->field_elems = (size_t)L->ntiles * L->nzq * 64 * (128 / es);

@@ -266,23 +266,26 @@ struct BcBoxes {
 };
 
 // ---- LDS working set of one solve wave -------------------------------------
-// Tiles are streamed through the wave in diagonal (wavefront) order of the
-// sweep direction; a tile enters the stream only if it or a face neighbour
-// changed since its last visit (exact: an update of unchanged inputs returns
-// the node's current value).  Per-tile clocks live in LDS.
+// The stream of a sweep is a sequence of positions of kb z-bricks each: the
+// z-blocks (tile, tz) that need an update, tiles in diagonal (wavefront)
+// order of the sweep direction and, inside a tile, a run of consecutive
+// z-blocks from the first one whose inputs changed to the column's end (a
+// block's z-upwind neighbour is still in flight when the next block is
+// decided, so a run never stops early).  Bubble positions keep an upwind x/y
+// neighbour's visit >= vis positions back (halo visibility).  Per-block
+// clocks live in LDS.
 template <typename R>
 struct Smem {
     int *box;                    // BC boxes [MCEIK_MAX_SRC][6]
-    float *cc;                   // cell cache [3][CC_MAX]            (SLOWMODE 2)
-    int *order;                  // diagonal order: txs | tys << 16   [ntiles]
-    int *lastproc, *lastchg;     // stream clock of the last visit / last visit with a change
-    unsigned short *u0ep;        // iteration+1 of the last u0 store of the tile
-    int *ring;                   // stream entries of positions p & 3: tx | ty << 12 | u0 flag << 24
-    u4v *cinfo;                  // [4][64] column info of every lane for positions p & 3
+    float *cc;                   // cell cache [nr][ccb]                   (SLOWMODE 2)
+    int *order;                  // diagonal tile order: txs | tys << 16   [ntiles]
+    int *lastproc, *lastchg;     // per z-block stream clock of the last visit / last visit with a change
+    unsigned short *u0ep;        // per z-block iteration+1 of the last u0 store
+    int *ring;                   // per position (mod nr): block entry tx | ty << 12 | tz << 24, bubble -1
+    int *scratch;                // debug counters
+    u4v *cinfo;                  // [nr][64] column info of every lane per position
     R *sf, *shx, *shy;           // staged slowness*h (modes 0,1) and halos
 };
-
-#define CC_MAX MCEIK_CC_MAX      // floats per cell-cache buffer (3 buffers)
 
 template <typename R>
 __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *base)
@@ -296,7 +299,8 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     S.lastproc = reinterpret_cast<int *>(base + off[3]);
     S.lastchg = reinterpret_cast<int *>(base + off[4]);
     S.u0ep = reinterpret_cast<unsigned short *>(base + off[5]);
-    S.ring = reinterpret_cast<int *>(base + off[7]);
+    S.ring = reinterpret_cast<int *>(base + off[6]);
+    S.scratch = reinterpret_cast<int *>(base + off[7]);
     S.sf = reinterpret_cast<R *>(base + off[8]);
     S.shx = reinterpret_cast<R *>(base + off[9]);
     S.shy = reinterpret_cast<R *>(base + off[10]);
@@ -304,44 +308,53 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     return S;
 }
 
-// Position of a lane in the stream of one sweep: stream position sp (tile
-// ordinal within the sweep) and z-brick zbs, advanced one virtual brick per
-// macro step.
+// Position of a lane in the stream of one sweep: stream position sp, its ring
+// slot ri = sp mod nr, and the step zbs (0..kb-1) inside the position,
+// advanced one virtual brick per macro step.
 struct Pos {
-    int vb, sp, zbs;
+    int vb, sp, zbs, ri;
 };
-__device__ __forceinline__ void pos_init(Pos &p, int vb, int sb)
+__device__ __forceinline__ void pos_init(Pos &p, int vb, const FsmLaunch &L)
 {
     p.vb = vb;
     const int v = vb < 0 ? 0 : vb;
-    p.sp = v / sb; p.zbs = v - p.sp * sb;
+    p.sp = v / L.kb; p.zbs = v - p.sp * L.kb;
+    p.ri = p.sp % L.nr;
 }
-__device__ __forceinline__ void pos_adv(Pos &p, int sb)
+__device__ __forceinline__ void pos_adv(Pos &p, const FsmLaunch &L)
 {
-    if (p.vb >= 0 && ++p.zbs == sb) {
+    if (p.vb >= 0 && ++p.zbs == L.kb) {
         p.zbs = 0; p.sp++;
+        if (++p.ri == L.nr) p.ri = 0;
     }
     p.vb++;
 }
-__device__ __forceinline__ bool pos_valid(const Pos &p, int nstream, int nzb)
+__device__ __forceinline__ bool pos_valid(const Pos &p, int nstream)
 {
-    return p.vb >= 0 && p.sp < nstream && p.zbs < nzb;
+    return p.vb >= 0 && p.sp < nstream;
 }
 
 // Column flags (written at admission, per lane and position) and brick flags.
 enum {
     C_ACT = 1,      // column inside the grid
-    C_U0 = 2,       // first visit of the tile in this iteration: store u0
+    C_U0 = 2,       // first visit of the z-block in this iteration: store u0
     C_PART = 4,     // tile cut by the grid's x or y end (generic path)
     C_00 = 8,       // column of node (0,0,0) (ierr, generic path)
     C_BC = 16,      // column crosses a boundary-condition box in x and y
-    F_VALID = 32, F_FIRST = 64, F_LAST = 128, F_SLOW = 256
+    C_BLK = 32,     // the position holds a z-block (not a bubble)
+    C_ZH = 64,      // run start inside the column: the z-upwind value comes from HBM
+    F_VALID = 128, F_FIRST = 256, F_LAST = 512, F_SLOW = 1024, F_ZH = 2048
 };
+// column info word w: flags (bits 0-6) | tz << 8 | (signed) cell-cache base << 16
+__device__ __forceinline__ int ci_tz(unsigned w) { return (int)((w >> 8) & 0xff); }
+__device__ __forceinline__ int ci_ccb(unsigned w) { return (int)w >> 16; }
 
 // What a lane needs about one of its bricks.
 struct BInfo {
     uint32_t seg;            // byte offset (u buffer) of the own segment (OOB if none)
-    int zb8, fl, ccb, sp;    // fl: C_* | F_*; ccb: cell-cache index of the brick (SLOWMODE 2)
+    int zb8, fl, ccb, ri;    // fl: C_* | F_*; ccb: cell-cache index of the brick (SLOWMODE 2); ri: ring slot
+    int bid;                 // z-block id (stamps)
+    int clk;                 // stream position of the brick (stamps)
     int bcm;                 // BC z-slots of the segment (generic path)
 };
 
@@ -352,16 +365,23 @@ __device__ __forceinline__ void tile_cells(int t, int n, unsigned magic, int &c0
     c0 = (int)(((unsigned)a * magic) >> 20);
     nc = (int)(((unsigned)b * magic) >> 20) - c0 + 1;
 }
+// Cell range of z-block tz.
+__device__ __forceinline__ void block_zcells(const FsmLaunch &L, int tz, int &cz0, int &ncz)
+{
+    const int a = tz * L.kb * 8, b = min(a + L.kb * 8, L.nz) - 1;
+    cz0 = (int)(((unsigned)a * L.magic_rz) >> 20);
+    ncz = (int)(((unsigned)b * L.magic_rz) >> 20) - cz0 + 1;
+}
 
-// Column info of this lane for tile `entry` at stream position pos.  The x/y
+// Column info of this lane for block `entry` at ring slot ri.  The x/y
 // halo of a tile-edge lane is the neighbour column, or the lane's own column
 // where the grid ends (the reference's missing neighbour is the node itself:
 // the halo then holds exactly the node's old value); interior lanes: OOB.
 template <typename R>
-__device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc, int entry, int pos, int u0flag,
-                                           int lx, int ly, int lxs, int lys, int rx, int ry)
+__device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc, int entry, int ri, int u0flag,
+                                           int zh, int lx, int ly, int lxs, int lys, int rx, int ry)
 {
-    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
+    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff, tz = (entry >> 24) & 0xff;
     const int x = tx * 8 + lx, y = ty * 8 + ly;
     const uint32_t st = tile_bytes<R>(L);
     const uint32_t col = (uint32_t)(ty * L.ntx + tx) * st + (uint32_t)colpos(lx, ly) * 128u;
@@ -376,23 +396,26 @@ __device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc
         hy = (yn >= 0 && yn < L.ny) ? (uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)colpos(lx, yn & 7) * 128u
                                      : col;
     }
-    int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
+    int m = (x < L.nx && y < L.ny) ? (C_ACT | C_BLK) : C_BLK;
     if (u0flag) m |= C_U0;
+    if (zh) m |= C_ZH;
     if (tx * 8 + 8 > L.nx || ty * 8 + 8 > L.ny) m |= C_PART;
     if (x == 0 && y == 0) m |= C_00;
     for (int k = 0; k < bc.n; k++) {
         const int *q = bc.box + 6 * k;
         if (x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]) m |= C_BC;
     }
-    int cx0, ncxt, cy0, ncyt;
+    int cx0, ncxt, cy0, ncyt, cz0, nczb;
     tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
     tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
+    block_zcells(L, tz, cz0, nczb);
     const int xc = x < L.nx ? x : L.nx - 1, yc = y < L.ny ? y : L.ny - 1;
     const int cxl = (int)(((unsigned)xc * L.magic_rx) >> 20) - cx0;
     const int cyl = (int)(((unsigned)yc * L.magic_ry) >> 20) - cy0;
-    const int ccb = (pos % 3) * CC_MAX + (cyl * ncxt + cxl) * L.ncz;
+    // cell of node z: cc[ccb + cz] with cz the absolute z cell
+    const int ccb = ri * L.ccb + (cyl * ncxt + cxl) * nczb - cz0;
     u4v v;
-    v.x = col; v.y = hx; v.z = hy; v.w = (unsigned)(m | (ccb << 8));
+    v.x = col; v.y = hx; v.z = hy; v.w = (unsigned)(m | (tz << 8) | (ccb << 16));
     return v;
 }
 
@@ -402,22 +425,25 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
 {
     BInfo b;
     const int lane = threadIdx.x;
-    const bool valid = pos_valid(p, nstream, L.nzb);
-    const u4v ci = S.cinfo[(p.sp & 3) * 64 + lane];
-    const int zb = valid ? (RZ ? L.nzb - 1 - p.zbs : p.zbs) : 0;
-    const uint32_t zoff = zoff_bytes<R>(zb);
-    b.seg = valid ? ci.x + zoff : OOB;
-    b.zb8 = zb * 8;
-    b.sp = p.sp;
-    const int meta = (int)ci.w;
-    int fl = valid ? ((meta & 0xff) | F_VALID) : 0;
+    const u4v ci = S.cinfo[p.ri * 64 + lane];
+    const int e = S.ring[p.ri];
+    const unsigned meta = ci.w;
+    const int tz = ci_tz(meta);
+    const int zb = tz * L.kb + (RZ ? L.kb - 1 - p.zbs : p.zbs);
+    const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < L.nzb;
+    b.seg = valid ? ci.x + zoff_bytes<R>(zb) : OOB;
+    b.zb8 = valid ? zb * 8 : 0;
+    b.ri = p.ri;
+    b.clk = p.sp;
+    b.bid = tz * L.ntiles + (e & 0xfff) + ((e >> 12) & 0xfff) * L.ntx;
+    int fl = valid ? (int)((meta & 0x7f) | F_VALID) : 0;
     if (zb == (RZ ? L.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : L.nzb - 1)) fl |= F_LAST;
+    if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
     bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && b.zb8 + 8 > L.nz);
     b.bcm = 0;
     if (__any(fl & C_BC)) {
         // BC z-slots of this column segment (rare: columns through a source box)
-        const int e = S.ring[p.sp & 3];
         const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
         unsigned m = 0;
         if (fl & C_BC) {
@@ -435,21 +461,36 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
     }
     if (slow) fl |= F_SLOW;
     b.fl = fl;
-    b.ccb = (meta >> 8) + (ZSH >= 0 ? (b.zb8 >> (ZSH < 0 ? 0 : ZSH)) : 0);
+    b.ccb = ci_ccb(meta) + (ZSH >= 0 ? (b.zb8 >> (ZSH < 0 ? 0 : ZSH)) : 0);
     return b;
 }
 
-// Offsets of lane col_lane's segment and halos at stream position p (prefetch).
+// Offsets of lane col_lane's segment and halos at stream position p (prefetch),
+// and of its z-upwind node when the brick starts a run inside the column.
 template <typename R, bool RZ>
 __device__ __forceinline__ void seg_offsets(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
-                                            uint32_t &seg, uint32_t &hx, uint32_t &hy, int col_lane)
+                                            uint32_t &seg, uint32_t &hx, uint32_t &hy, uint32_t &zh, int col_lane)
 {
-    const bool valid = pos_valid(p, nstream, L.nzb);
-    const u4v ci = S.cinfo[(p.sp & 3) * 64 + col_lane];
-    const uint32_t zoff = zoff_bytes<R>(RZ ? L.nzb - 1 - p.zbs : p.zbs);
+    const u4v ci = S.cinfo[p.ri * 64 + col_lane];
+    const unsigned meta = ci.w;
+    const int zb = ci_tz(meta) * L.kb + (RZ ? L.kb - 1 - p.zbs : p.zbs);
+    const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < L.nzb;
+    const uint32_t zoff = zoff_bytes<R>(zb);
     seg = valid ? ci.x + zoff : OOB;
     hx = valid ? ci.y + zoff : OOB;
     hy = valid ? ci.z + zoff : OOB;
+    const int zu = RZ ? zb * 8 + 8 : zb * 8 - 1;             // z-upwind node of the brick's first slot
+    zh = (valid && (meta & C_ZH) && p.zbs == 0)
+             ? ci.x + zoff_bytes<R>(zu >> 3) + (uint32_t)(zu & 7) * (uint32_t)sizeof(R) : OOB;
+}
+
+__device__ __forceinline__ float bload1(Rsrc r, uint32_t off, float)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ double bload1(Rsrc r, uint32_t off, double)
+{
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
 
 template <typename R, int SLOWMODE>
@@ -470,7 +511,7 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R> 
     if (SLOWMODE == 0) {
         bload8(sr, b.seg, s);
     } else {
-        const int e = S.ring[b.sp & 3];
+        const int e = S.ring[b.ri];
         const uint32_t mx = L.magic_rx, my = L.magic_ry, mz = L.magic_rz;
         int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
         x = x < L.nx ? x : L.nx - 1; y = y < L.ny ? y : L.ny - 1;
@@ -487,110 +528,163 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R> 
     }
 }
 
-// Cell cache (SLOWMODE 2): the slowness cells a tile touches (2 x 2 x ncz at
-// nref = 4), three buffers indexed by stream position mod 3.  Loads for the
-// tile at position k are issued two macro steps before lane (0,0) enters it
-// and written at the end of that step; the buffer they replace (position k-3)
-// has no reader left (sb >= 11).  fp32 entries hold f = s*h (the product the
+// Cell cache (SLOWMODE 2): the slowness cells of a z-block (2 x 2 x 8 at
+// nref = 4, kb = 4), one buffer per ring slot.  Loads for the block at
+// position k are issued two macro steps before lane (0,0) enters it and
+// written at the end of that step; the slot's previous block (position
+// k - nr) has no reader left.  fp32 entries hold f = s*h (the product the
 // update uses, rounded once as before); fp64 entries hold s.
-__device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int entry, float (&v)[CC_MAX / 64], int &size)
+template <int CCR>
+__device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int entry, float (&v)[CCR], int &size)
 {
     const int lane = threadIdx.x;
-    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
-    int cx0, ncxt, cy0, ncyt;
+    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff, tz = (entry >> 24) & 0xff;
+    int cx0, ncxt, cy0, ncyt, cz0, nczb;
     tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
     tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
-    size = entry >= 0 ? ncxt * ncyt * L.ncz : 0;
+    block_zcells(L, tz, cz0, nczb);
+    size = entry >= 0 ? ncxt * ncyt * nczb : 0;
 #pragma unroll
-    for (int r = 0; r < CC_MAX / 64; r++) {
+    for (int r = 0; r < CCR; r++) {
         const int idx = lane + 64 * r;
-        const int cz = idx % L.ncz, t = idx / L.ncz;
+        const int cz = idx % nczb, t = idx / nczb;
         const int cyl = t / ncxt, cxl = t - cyl * ncxt;
-        const uint32_t off = (uint32_t)(((cz * L.ncy + cy0 + cyl) * L.ncx) + cx0 + cxl) * 4u;
+        const uint32_t off = (uint32_t)((((cz0 + cz) * L.ncy + cy0 + cyl) * L.ncx) + cx0 + cxl) * 4u;
         v[r] = bload1f(sr, idx < size ? off : OOB);
     }
 }
-template <typename R>
-__device__ __forceinline__ void cc_write(float *cc, int buf, const float (&v)[CC_MAX / 64], int size, float h)
+template <typename R, int CCR>
+__device__ __forceinline__ void cc_write(const FsmLaunch &L, float *cc, int ri, const float (&v)[CCR], int size,
+                                         float h)
 {
     const int lane = threadIdx.x;
 #pragma unroll
-    for (int r = 0; r < CC_MAX / 64; r++) {
+    for (int r = 0; r < CCR; r++) {
         const int idx = lane + 64 * r;
-        if (idx < size) cc[buf * CC_MAX + idx] = sizeof(R) == 4 ? v[r] * h : v[r];
+        if (idx < size) cc[ri * L.ccb + idx] = sizeof(R) == 4 ? v[r] * h : v[r];
     }
 }
 
-// Choose the next tile of the stream: the first tile (diagonal order from
-// `cursor`) that changed at its last visit, has a face neighbour that changed
-// since, or has a sweep-upwind neighbour still in flight (whose changes are
-// not known yet).  64 candidates are judged per ballot.  Returns the ring
-// entry (tx | ty << 12) or -1 when the sweep has no tile left.
-template <typename R>
-__device__ int choose_tile(const FsmLaunch &L, const Smem<R> &S, int &cursor, int infl0, int infl1, int rx, int ry)
+// Stream state of a sweep (wave-uniform): the next tile (diagonal order) to
+// scan, the run in progress (tile, next sweep-relative z-block, first block
+// of the run) and the bubbles still owed before it.
+struct Stream {
+    int cursor, tile, k, k0, wait;
+};
+
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Decide stream position `pos` (global clock C = clock0 + pos): a z-block
+// (returns its entry, *zh = run start inside the column), a bubble (-1) or the
+// end of the sweep (-2).  A z-block needs an update iff it changed at its
+// last visit, a face neighbour changed since, or a sweep-upwind x/y neighbour
+// is still in flight (its changes are not known yet); otherwise its update
+// would recompute every node from unchanged inputs and return the current
+// value.  Once a run starts, the next block's z-upwind neighbour is in flight,
+// so the run covers the rest of the column.
+template <typename R, bool RZ>
+__device__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, int rx, int ry, int &zh)
 {
     const int lane = threadIdx.x;
-    while (cursor < L.ntiles) {
-        const int k = cursor + lane;
-        bool dirty = false;
-        int entry = 0;
-        if (k < L.ntiles) {
-            const int o = S.order[k];
-            const int txs = o & 0xffff, tys = o >> 16;
-            const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
-            const int id = ty * L.ntx + tx;
-            const int lp = S.lastproc[id];
-            dirty = S.lastchg[id] >= lp;
-            if (tx > 0) dirty |= S.lastchg[id - 1] > lp;
-            if (tx < L.ntx - 1) dirty |= S.lastchg[id + 1] > lp;
-            if (ty > 0) dirty |= S.lastchg[id - L.ntx] > lp;
-            if (ty < L.nty - 1) dirty |= S.lastchg[id + L.ntx] > lp;
-            const int xu = txs > 0 ? id + (rx ? 1 : -1) : -2;
-            const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -2;
-            dirty |= xu == infl0 || xu == infl1 || yu == infl0 || yu == infl1;
-            entry = tx | (ty << 12);
+    const int nt = L.ntiles, nzk = L.nzk;
+    zh = 0;
+    if (st.tile < 0) {
+        while (st.cursor < nt) {
+            const int k = st.cursor + lane;
+            int k0 = nzk, entry = 0;
+            if (k < nt) {
+                const int o = S.order[k];
+                const int txs = o & 0xffff, tys = o >> 16;
+                const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+                const int id = ty * L.ntx + tx;
+                const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
+                const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -1;
+                entry = tx | (ty << 12);
+                for (int kz = 0; kz < nzk; kz++) {
+                    const int tz = RZ ? nzk - 1 - kz : kz;
+                    const int b = tz * nt + id;
+                    const int lp = S.lastproc[b];
+                    bool d = S.lastchg[b] >= lp;
+                    if (tx > 0) d |= S.lastchg[b - 1] > lp;
+                    if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
+                    if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
+                    if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
+                    if (tz > 0) d |= S.lastchg[b - nt] > lp;
+                    if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
+                    if (xu >= 0) d |= S.lastproc[tz * nt + xu] > C - L.infl;
+                    if (yu >= 0) d |= S.lastproc[tz * nt + yu] > C - L.infl;
+                    if (d) { k0 = kz; break; }
+                }
+            }
+            const unsigned long long m = __ballot(k0 < nzk);
+            if (m) {
+                const int first = __builtin_ctzll(m);
+                st.cursor += first + 1;
+                st.tile = __builtin_amdgcn_readfirstlane(__shfl(entry, first, 64));
+                st.k0 = st.k = __builtin_amdgcn_readfirstlane(__shfl(k0, first, 64));
+                break;
+            }
+            st.cursor += 64;
         }
-        const unsigned long long m = __ballot(dirty);
-        if (m) {
-            const int first = __builtin_ctzll(m);
-            cursor += first + 1;
-            return __shfl(entry, first, 64);
+        if (st.tile < 0) return -2;
+        // bubbles before the run: block k sits at position pos + wait + (k - k0),
+        // which must be >= vis positions after its upwind x/y neighbours' visits
+        const int tx = st.tile & 0xfff, ty = st.tile >> 12;
+        const int txs = rx ? L.ntx - 1 - tx : tx, tys = ry ? L.nty - 1 - ty : ty;
+        const int id = ty * L.ntx + tx;
+        int need = 0;
+        for (int kz = st.k0 + lane; kz < nzk; kz += 64) {
+            const int tz = RZ ? nzk - 1 - kz : kz;
+            int p = -0x40000000;
+            if (txs > 0) p = max(p, S.lastproc[tz * nt + id + (rx ? 1 : -1)]);
+            if (tys > 0) p = max(p, S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)]);
+            need = max(need, p + L.vis - (kz - st.k0) - C);
         }
-        cursor += 64;
+        st.wait = __builtin_amdgcn_readfirstlane(wave_max(need));
     }
-    return -1;
+    if (st.wait > 0) {
+        st.wait--;
+        return -1;
+    }
+    const int kz = st.k;
+    zh = kz == st.k0 && kz > 0;
+    const int tz = RZ ? nzk - 1 - kz : kz;
+    const int e = st.tile | (tz << 24);
+    if (++st.k == nzk) st.tile = -1;
+    return e;
 }
 
-// Admit the chosen tile at stream position pos: every lane writes its column
-// info, lane 0 the ring entry and the tile's clocks.
+// Admit stream position pos (ring slot ri): a z-block (every lane writes its
+// column info, lane 0 the ring entry and the block's clocks) or a bubble.
 template <typename R>
-__device__ __forceinline__ void admit_tile(const FsmLaunch &L, const Smem<R> &S, const BcBoxes &bc, int entry, int pos,
-                                           int clock, int it, int lx, int ly, int lxs, int lys, int rx, int ry)
+__device__ __forceinline__ void admit(const FsmLaunch &L, const Smem<R> &S, const BcBoxes &bc, int entry, int zh,
+                                      int ri, int clock, int it, int lx, int ly, int lxs, int lys, int rx, int ry)
 {
-    const int id = (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
-    const int u0flag = S.u0ep[id] != (unsigned short)(it + 1);
-    const u4v ci = column_info<R>(L, bc, entry, pos, u0flag, lx, ly, lxs, lys, rx, ry);
-    asm volatile("" ::: "memory");
-    S.cinfo[(pos & 3) * 64 + threadIdx.x] = ci;
-#ifdef MCEIK_BLOCK_STATS
-    if (threadIdx.x == 0 && L.visit_stats) {
-        atomicAdd(L.visit_stats + 2, (unsigned long long)__builtin_popcount(((unsigned *)S.ring)[4 + (pos & 3)]));
-        ((unsigned *)S.ring)[4 + (pos & 3)] = 0;
+    u4v ci;
+    int bid = 0, u0flag = 0;
+    if (entry >= 0) {
+        const int tz = (entry >> 24) & 0xff;
+        bid = tz * L.ntiles + (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
+        u0flag = S.u0ep[bid] != (unsigned short)(it + 1);
+        ci = column_info<R>(L, bc, entry, ri, u0flag, zh, lx, ly, lxs, lys, rx, ry);
+    } else {
+        ci.x = OOB; ci.y = OOB; ci.z = OOB; ci.w = 0;
     }
-#endif
+    asm volatile("" ::: "memory");
+    S.cinfo[ri * 64 + threadIdx.x] = ci;
     if (threadIdx.x == 0) {
-        S.u0ep[id] = (unsigned short)(it + 1);
-        S.lastproc[id] = clock;
-        S.ring[pos & 3] = entry | (u0flag << 24);
+        if (entry >= 0) {
+            S.u0ep[bid] = (unsigned short)(it + 1);
+            S.lastproc[bid] = clock;
+        }
+        S.ring[ri] = entry;
     }
     asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ int ring_tile(const FsmLaunch &L, const int *ring, int pos)
-{
-    if (pos < 0) return -1;
-    const int e = ring[pos & 3];
-    return (e & 0xfff) + ((e >> 12) & 0xfff) * L.ntx;
 }
 
 // min of two travel times.  Values in the field are never NaN or -0 (every
@@ -694,7 +788,7 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
 // missing x/y neighbours are already its own old values (column_info).
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC>
 __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, R (&c)[8],
-                                             R (&n)[8], R (&r)[8], int lx, int ly, int rx, int ry,
+                                             R (&n)[8], R (&r)[8], R zc, int lx, int ly, int rx, int ry,
                                              bool &changed, bool &nc, int &ierr_last)
 {
     const int lane = threadIdx.x;
@@ -702,13 +796,16 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
     const int fl = b0.fl;
     bool xp = true, xn = true, yp = true, yn = true, act = true;
     if (GENERIC) {
-        const int e = S.ring[b0.sp & 3];
+        const int e = S.ring[b0.ri];
         const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
         const bool xlo = x > 0, xhi = x < L.nx - 1, ylo = y > 0, yhi = y < L.ny - 1;
         xp = rx ? xhi : xlo; xn = rx ? xlo : xhi; yp = ry ? yhi : ylo; yn = ry ? ylo : yhi;
         act = (fl & C_ACT) != 0;
     }
     const bool first = (fl & F_FIRST) != 0, last = (fl & F_LAST) != 0;
+    // z-upwind value of slot 0: the previous brick of the lane's sequence, or
+    // (run start inside the column) the node loaded from HBM
+    const R zprev = (fl & F_ZH) ? zc : r[RZ ? 0 : 7];
     int aup = ((lane - 8) & 63) * 4, adn = ((lane + 8) & 63) * 4;
     asm volatile("" : "+v"(aup), "+v"(adn));
     // fast fp32 path over the LDS cell cache: f, f*f, 2f*f per cell
@@ -736,10 +833,10 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
             const int zabs = b0.zb8 + pj;
             const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
             const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
-            zup = zp_ex ? (j > 0 ? r[pprev] : r[RZ ? 0 : 7]) : self;
+            zup = zp_ex ? (j > 0 ? r[pprev] : zprev) : self;
             zdn = zn_ex ? (j < 7 ? c[pnext] : n[RZ ? 7 : 0]) : self;
         } else {
-            zup = j > 0 ? r[pprev] : (first ? self : r[RZ ? 0 : 7]);
+            zup = j > 0 ? r[pprev] : (first ? self : zprev);
             zdn = j < 7 ? c[pnext] : (last ? self : n[RZ ? 7 : 0]);
         }
         const R uz = fmin_(zup, zdn);
@@ -763,9 +860,9 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
 }
 
 // One Gauss-Seidel sweep over the grid in direction (rx, ry, RZ): only the
-// tiles admitted by choose_tile are visited.  Returns the number of stream
-// positions used (the clock advance).
-template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH>
+// z-blocks admitted by decide() are visited.  Returns the number of stream
+// positions used (z-blocks and bubbles).
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
                                      const Smem<R> &S, int rx, int ry, int it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned long long &visited,
@@ -774,46 +871,59 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
-    const R hr = (R)L.h, T = (R)L.conv_thresh;
-    const int sb = L.sb;
+    const R hr = (R)L.h;
+    const int kb = L.kb;
 
     const int hxsel = lxs == 7, hysel = lys >= 4;
 
     // stream bookkeeping (wave-uniform)
-    int cursor = 0, ndecided = 0, nstream = 0x7fffffff;
-    {
-        const int e = choose_tile<R>(L, S, cursor, -1, -1, rx, ry);
-        if (e < 0) return 0;                                // nothing changed near any tile: skip the sweep
-        admit_tile<R>(L, S, bc, e, 0, clock0, it, lx, ly, lxs, lys, rx, ry);
-        ndecided = 1;
-    }
+    Stream st;
+    st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8], hxn[8], hyn[8];
-    float ccv[CC_MAX / 64];
+    R zc, zn, zq;                    // z-upwind values of run starts (vb, vb+1, vb+2)
+    float ccv[CCR];
     int ccsize = 0;
+    // prologue decisions: the positions of lane (0,0)'s bricks 0 and 1 (one
+    // position, or two when kb = 1); the loop then decides position (B+2)/kb
+    int ndecided = 0, nstream = 0x7fffffff, dri = 0;
+    for (int pos = 0; pos <= (kb == 1 ? 1 : 0); pos++) {
+        int zh;
+        const int e = decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
+        if (e == -2) {
+            if (pos == 0) return 0;                         // nothing changed near any block: skip the sweep
+            nstream = pos;
+            break;
+        }
+        admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry);
+        if (SLOWMODE == 2 && e >= 0) {
+            cc_issue<CCR>(L, sr, e, ccv, ccsize);
+            cc_write<R, CCR>(L, S.cc, dri, ccv, ccsize, (float)L.h);
+        }
+        ndecided = pos + 1;
+        if (++dri == L.nr) dri = 0;
+    }
+    asm volatile("" ::: "memory");
     Pos p1;
-    pos_init(p1, -d, sb);
+    pos_init(p1, -d, L);
     BInfo b0 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
     // prologue: c = brick(vb0), n = brick(vb0+1); stage f and halos of vb0
     bload8(ur, b0.seg, c);
-    if (SLOWMODE == 2) {
-        cc_issue(L, sr, S.ring[0] & 0xffffff, ccv, ccsize);
-        cc_write<R>(S.cc, 0, ccv, ccsize, (float)L.h);
-    } else {
-        prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
-    }
+    if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
     {
-        uint32_t s_, hx_, hy_;
-        seg_offsets<R, RZ>(L, S, p1, nstream, s_, hx_, hy_, lane);
+        uint32_t s_, hx_, hy_, zh_;
+        seg_offsets<R, RZ>(L, S, p1, nstream, s_, hx_, hy_, zh_, lane);
         bload8(ur, hx_, hxq);
         bload8(ur, hy_, hyq);
+        zc = bload1(ur, zh_, R());
     }
-    pos_adv(p1, sb);
+    pos_adv(p1, L);
     {
-        uint32_t s1, hx_, hy_;
-        seg_offsets<R, RZ>(L, S, p1, nstream, s1, hx_, hy_, lane);
+        uint32_t s1, hx_, hy_, zh_;
+        seg_offsets<R, RZ>(L, S, p1, nstream, s1, hx_, hy_, zh_, lane);
         bload8(ur, s1, n);
         bload8(ur, hx_, hxn);            // halos of vb+1: one more step in flight
         bload8(ur, hy_, hyn);
+        zn = bload1(ur, zh_, R());
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -832,82 +942,72 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     for (int i = 0; i < 8; i++) { hxq[i] = hxn[i]; hyq[i] = hyn[i]; }
     asm volatile("" ::: "memory");
 
-    int ph = 2 % sb;                 // (B + 2) mod sb: 0 when lane (0,0)'s vb+2 starts a new position
+    int ph = 2 % kb;                 // (B + 2) mod kb: 0 when lane (0,0)'s vb+2 starts a new position
     for (int B = 0;; B++) {
         // ---- stream decision for the position lane (0,0) prefetches next
         bool ccfill = false;
+        int ccri = 0;
         if (ph == 0 && nstream == 0x7fffffff) {
             const int pos = ndecided;
-            const int e = choose_tile<R>(L, S, cursor, ring_tile(L, S.ring, pos - 1), ring_tile(L, S.ring, pos - 2),
-                                         rx, ry);
-            if (e < 0) {
+            int zh;
+            const int e = decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
+            if (e == -2) {
                 nstream = pos;
             } else {
-                admit_tile<R>(L, S, bc, e, pos, clock0 + pos, it, lx, ly, lxs, lys, rx, ry);
-                ndecided = pos + 1;
-                if (SLOWMODE == 2) {
-                    cc_issue(L, sr, e, ccv, ccsize);
+                admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry);
+                if (SLOWMODE == 2 && e >= 0) {
+                    cc_issue<CCR>(L, sr, e, ccv, ccsize);
                     ccfill = true;
+                    ccri = dri;
                 }
+                ndecided = pos + 1;
+                if (++dri == L.nr) dri = 0;
             }
         }
-        if (nstream != 0x7fffffff && B >= nstream * sb + 14) break;
+        if (nstream != 0x7fffffff && B >= nstream * kb + 14) break;
         // ---- prefetch: own segment and halos of vb+2 (halos are staged at
-        // the end of the next step: two steps of latency cover, MCEIK_MIN_SB
-        // = 12), slowness of vb+1
+        // the end of the next step: two steps of latency cover), slowness of vb+1
         const BInfo b1 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
         {
             Pos p2 = p1;
-            pos_adv(p2, sb);
-            uint32_t s2, hx_, hy_;
-            seg_offsets<R, RZ>(L, S, p2, nstream, s2, hx_, hy_, lane);
+            pos_adv(p2, L);
+            uint32_t s2, hx_, hy_, zh_;
+            seg_offsets<R, RZ>(L, S, p2, nstream, s2, hx_, hy_, zh_, lane);
             bload8(ur, s2, q);
             bload8(ur, hx_, hxn);
             bload8(ur, hy_, hyn);
+            zq = bload1(ur, zh_, R());
         }
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
 
         // ---- the 8 z-slots of the current brick
         bool changed = false, nc = false;
         if (__any(b0.fl & F_SLOW))
-            brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, lx, ly, rx, ry, changed, nc,
+            brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                            ierr_last);
         else
-            brick_update<R, SLOWMODE, FAST, RZ, ZSH, false>(L, S, b0, c, n, r, lx, ly, rx, ry, changed, nc,
+            brick_update<R, SLOWMODE, FAST, RZ, ZSH, false>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                             ierr_last);
         const bool val = (b0.fl & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
+        visited += (unsigned)__builtin_amdgcn_readfirstlane(val ? 1 : 0);   // bricks (lane (0,0) sees each once)
         if (L.visit_stats) {                                // wave-uniform; SALU popcounts
             segs += __builtin_popcountll(__ballot(val && (b0.fl & C_ACT)));
-#ifdef MCEIK_BLOCK_STATS
-            // debug: changed 4-brick z blocks per tile visit (ring slot sp & 3)
-            if (changed) atomicOr((unsigned *)(S.ring + 4 + (b0.sp & 3)), 1u << (b0.zb8 >> 5));
-#else
             segs_changed += __builtin_popcountll(__ballot(changed));
-#endif
         }
 
-        // ---- write-back, u0 at a tile's first visit of the iteration, change stamps
+        // ---- write-back, u0 at a block's first visit of the iteration, change stamps
         bstore8(ur, changed ? b0.seg : OOB, r);
         {
             R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
-            bstore8(u0r, (m < T && (b0.fl & C_U0)) ? b0.seg : OOB, c);
+            bstore8(u0r, (m < (R)L.conv_thresh && (b0.fl & C_U0)) ? b0.seg : OOB, c);
         }
-        {
-            // lanes sit on at most 3 stream positions: lane (0,0)'s and the two before
-            const int sp0 = __builtin_amdgcn_readfirstlane(b0.sp);
-#pragma unroll
-            for (int back = 0; back < 3; back++) {
-                const int pos = sp0 - back;
-                const bool mine = val && b0.sp == pos;
-                if (__any(changed && mine) && lane == 0) S.lastchg[ring_tile(L, S.ring, pos)] = clock0 + pos;
-            }
-        }
+        if (changed) S.lastchg[b0.bid] = clock0 + b0.clk;   // lanes of one block write the same value
         asm volatile("" ::: "memory");
         // ---- stage the prefetched slowness/halos of vb+1 for the next step
         if (SLOWMODE == 2) {
-            if (ccfill) cc_write<R>(S.cc, (ndecided - 1) % 3, ccv, ccsize, (float)L.h);
+            if (ccfill) cc_write<R, CCR>(L, S.cc, ccri, ccv, ccsize, (float)L.h);
         } else {
 #pragma unroll
             for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
@@ -923,32 +1023,34 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; hxq[i] = hxn[i]; hyq[i] = hyn[i]; }
+        zc = zn; zn = zq;
         b0 = b1;
-        pos_adv(p1, sb);
-        if (++ph == sb) ph = 0;
+        pos_adv(p1, L);
+        if (++ph == kb) ph = 0;
     }
-    visited += (unsigned long long)nstream;
     return nstream;
 }
 
 // End-of-iteration check of the nodes below T (run only when no node >= T
-// changed): the tiles that changed in this iteration (lastchg >= the
+// changed): the z-blocks that changed in this iteration (lastchg >= the
 // iteration's first clock); u0 was stored at their first visit.
 template <typename R>
 __device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int clock_it, bool &notconv)
 {
     const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
     const R T = (R)L.conv_thresh, tolr = (R)L.tol;
-    for (int base = 0; base < L.ntiles; base += 64) {
+    for (int base = 0; base < L.nblocks; base += 64) {
         const int k = base + lane;
-        const bool flag = k < L.ntiles && S.lastchg[k] >= clock_it;
+        const bool flag = k < L.nblocks && S.lastchg[k] >= clock_it;
         unsigned long long m = __ballot(flag);
         while (m) {
-            const int id = base + __builtin_ctzll(m);
+            const int bid = base + __builtin_ctzll(m);
             m &= m - 1;
+            const int tz = bid / L.ntiles, id = bid - tz * L.ntiles;
             const int tx = id % L.ntx, ty = id / L.ntx;
             const int x = tx * 8 + lx, y = ty * 8 + ly;
-            for (int zb = 0; zb < L.nzb; zb++) {
+            const int zend = min(tz * L.kb + L.kb, L.nzb);
+            for (int zb = tz * L.kb; zb < zend; zb++) {
                 const uint32_t seg = (uint32_t)id * tile_bytes<R>(L) + zoff_bytes<R>(zb) + (uint32_t)colpos(lx, ly) * 128u;
                 R u[8], v0[8];
                 bload8(ur, seg, u);
@@ -1064,7 +1166,7 @@ __device__ void build_order(const FsmLaunch &L, int *order)
     }
 }
 
-template <typename R, int SLOWMODE, bool FAST, int ZSH>
+template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR>
 __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1093,14 +1195,30 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
             slow_bytes = (uint32_t)(ncell * 4);
         }
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
-        for (int t = lane; t < L.ntiles; t += 64) {
-            S.lastproc[t] = -1; S.lastchg[t] = -1;       // every tile dirty for the first sweep
+        // Clocks before the first sweep: every block "visited" at -2 and
+        // unchanged since (-3), except the blocks holding boundary-condition
+        // nodes (changed at -1).  Exact: a block whose nodes and neighbours
+        // are all u_nan updates to u_nan (a1 == u_nan), so it needs no visit
+        // until a neighbour changes.  The stream clock starts at 64, so no
+        // initial visit counts as in flight.
+        for (int t = lane; t < L.nblocks; t += 64) {
+            S.lastproc[t] = -2; S.lastchg[t] = -3;
             S.u0ep[t] = 0;
         }
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
-        int iters = 0, ierr_last = 0, clock = 0;
+        if (lane == 0) {
+            for (int k = 0; k < bc.n; k++) {
+                const int *q = bc.box + 6 * k;
+                for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
+                    for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
+                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
+                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = -1;
+            }
+        }
+        asm volatile("" ::: "memory");
+        int iters = 0, ierr_last = 0, clock = 64;
         if (ok) {
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
@@ -1108,12 +1226,16 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                 const int clock_it = clock;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
+                    // positions used + a gap of infl: the previous sweep's visits are
+                    // never in flight (nor within vis) for the next one
                     if (sw & 4)
-                        clock += sweep<R, SLOWMODE, FAST, true, ZSH>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
-                                                                notconv, ierr_last, visited, segs, segs_changed);
+                        clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR>(
+                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last,
+                                              visited, segs, segs_changed);
                     else
-                        clock += sweep<R, SLOWMODE, FAST, false, ZSH>(L, ur, u0r, sr, bc, S, rx, ry, it, clock,
-                                                                 notconv, ierr_last, visited, segs, segs_changed);
+                        clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR>(
+                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last,
+                                              visited, segs, segs_changed);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
@@ -1189,46 +1311,47 @@ __global__ void from_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfiel
 }  // namespace
 
 // ---- host-side launchers (C++ linkage, used by capi.hip) ---------------------
-template <typename R, int SLOWMODE, bool FAST, int ZSH>
+template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR>
 static hipError_t launch_fsm(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     size_t lds = fsm_lds_bytes(L, sizeof(R));
-    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST, ZSH>), dim3(nwaves), dim3(64), lds, st, L);
+    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
 }
 
-template <typename R, int SLOWMODE, bool FAST, int ZSH>
+template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR>
 static int occupancy_of(size_t lds)
 {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST, ZSH>, 64, lds) ==
-                   hipSuccess ? nb : 1;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR>, 64,
+                                                        lds) == hipSuccess ? nb : 1;
 }
 
 // Kernel variant of a launch: slowness source, sqrt form, and (cell cache)
-// whether the z refinement is 4 (cell offsets of a brick's slots are constants).
+// whether the z refinement is 4 (cell offsets of a brick's slots are
+// constants) with at most 64 cells per z-block (one cell register per lane).
 static int variant(const FsmLaunch &L, int is_double)
 {
     const int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
     if (is_double) return 8 + mode * 2;
     if (mode != 2) return mode * 2;
-    return 4 + (L.fast_sqrt ? 1 : 0) + (L.nrz == 4 && L.fast_sqrt ? 2 : 0);
+    return 4 + (L.fast_sqrt ? 1 : 0) + (L.nrz == 4 && L.fast_sqrt && L.ccb <= 64 ? 2 : 0);
 }
 
 #define FSM_VARIANTS(X)                         \
-    X(0, float, 0, false, -1)                   \
-    X(2, float, 1, false, -1)                   \
-    X(4, float, 2, false, -1)                   \
-    X(5, float, 2, true, -1)                    \
-    X(7, float, 2, true, 2)                     \
-    X(8, double, 0, false, -1)                  \
-    X(10, double, 1, false, -1)                 \
-    X(12, double, 2, false, -1)
+    X(0, float, 0, false, -1, 1)                \
+    X(2, float, 1, false, -1, 1)                \
+    X(4, float, 2, false, -1, 4)                \
+    X(5, float, 2, true, -1, 4)                 \
+    X(7, float, 2, true, 2, 1)                  \
+    X(8, double, 0, false, -1, 1)               \
+    X(10, double, 1, false, -1, 1)              \
+    X(12, double, 2, false, -1, 4)
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st)
 {
     switch (variant(L, is_double)) {
-#define X(v, R, M, F, Z) case v: return launch_fsm<R, M, F, Z>(L, nwaves, st);
+#define X(v, R, M, F, Z, CR) case v: return launch_fsm<R, M, F, Z, CR>(L, nwaves, st);
         FSM_VARIANTS(X)
 #undef X
     default: return hipErrorInvalidValue;
@@ -1239,7 +1362,7 @@ int fsm_occupancy(const FsmLaunch &L, int is_double)
 {
     const size_t lds = fsm_lds_bytes(L, is_double ? 8 : 4);
     switch (variant(L, is_double)) {
-#define X(v, R, M, F, Z) case v: return occupancy_of<R, M, F, Z>(lds);
+#define X(v, R, M, F, Z, CR) case v: return occupancy_of<R, M, F, Z, CR>(lds);
         FSM_VARIANTS(X)
 #undef X
     default: return 1;
