@@ -373,15 +373,22 @@ __device__ __forceinline__ void block_zcells(const FsmLaunch &L, int tz, int &cz
     ncz = (int)(((unsigned)b * L.magic_rz) >> 20) - cz0 + 1;
 }
 
-// Column info of this lane for block `entry` at ring slot ri.  The x/y
-// halo of a tile-edge lane is the neighbour column, or the lane's own column
-// where the grid ends (the reference's missing neighbour is the node itself:
-// the halo then holds exactly the node's old value); interior lanes: OOB.
+// Column info of this lane for the tile of a run (entry: tx | ty << 12): the
+// own column and x/y halo offsets, the tile-level flags and the lane's cell
+// column (cyl * ncxt + cxl).  The x/y halo of a tile-edge lane is the
+// neighbour column, or the lane's own column where the grid ends (the
+// reference's missing neighbour is the node itself: the halo then holds
+// exactly the node's old value); interior lanes: OOB.
+struct ColTile {
+    int tile;                    // tx | ty << 12 of the cached tile, -1 none
+    uint32_t col, hx, hy;
+    int fl, cl;
+};
 template <typename R>
-__device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc, int entry, int ri, int u0flag,
-                                           int zh, int lx, int ly, int lxs, int lys, int rx, int ry)
+__device__ __forceinline__ void column_tile(const FsmLaunch &L, const BcBoxes &bc, int entry, int lx, int ly,
+                                            int lxs, int lys, int rx, int ry, ColTile &t)
 {
-    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff, tz = (entry >> 24) & 0xff;
+    const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
     const int x = tx * 8 + lx, y = ty * 8 + ly;
     const uint32_t st = tile_bytes<R>(L);
     const uint32_t col = (uint32_t)(ty * L.ntx + tx) * st + (uint32_t)colpos(lx, ly) * 128u;
@@ -396,27 +403,34 @@ __device__ __forceinline__ u4v column_info(const FsmLaunch &L, const BcBoxes &bc
         hy = (yn >= 0 && yn < L.ny) ? (uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)colpos(lx, yn & 7) * 128u
                                      : col;
     }
-    int m = (x < L.nx && y < L.ny) ? (C_ACT | C_BLK) : C_BLK;
-    if (u0flag) m |= C_U0;
-    if (zh) m |= C_ZH;
+    int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
     if (tx * 8 + 8 > L.nx || ty * 8 + 8 > L.ny) m |= C_PART;
     if (x == 0 && y == 0) m |= C_00;
     for (int k = 0; k < bc.n; k++) {
         const int *q = bc.box + 6 * k;
         if (x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]) m |= C_BC;
     }
-    int cx0, ncxt, cy0, ncyt, cz0, nczb;
+    int cx0, ncxt, cy0, ncyt;
     tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
     tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
-    block_zcells(L, tz, cz0, nczb);
     const int xc = x < L.nx ? x : L.nx - 1, yc = y < L.ny ? y : L.ny - 1;
     const int cxl = (int)(((unsigned)xc * L.magic_rx) >> 20) - cx0;
     const int cyl = (int)(((unsigned)yc * L.magic_ry) >> 20) - cy0;
-    // cell of node z: cc[ccb + cz] with cz the absolute z cell
-    const int ccb = ri * L.ccb + (cyl * ncxt + cxl) * nczb - cz0;
-    u4v v;
-    v.x = col; v.y = hx; v.z = hy; v.w = (unsigned)(m | (tz << 8) | (ccb << 16));
-    return v;
+    t.tile = entry & 0xffffff;
+    t.col = col; t.hx = hx; t.hy = hy;
+    t.fl = m;
+    t.cl = cyl * ncxt + cxl;
+}
+// Column info word of block tz of the cached tile at ring slot ri:
+// flags | tz << 8 | cell-cache base << 16, cell of node z = cc[base + z cell].
+__device__ __forceinline__ unsigned column_word(const FsmLaunch &L, const ColTile &t, int tz, int ri, int u0flag,
+                                                int zh)
+{
+    int cz0, nczb;
+    block_zcells(L, tz, cz0, nczb);
+    const int ccb = ri * L.ccb + t.cl * nczb - cz0;
+    const int m = t.fl | C_BLK | (u0flag ? C_U0 : 0) | (zh ? C_ZH : 0);
+    return (unsigned)(m | (tz << 8) | (ccb << 16));
 }
 
 template <typename R, bool RZ, int ZSH>
@@ -660,18 +674,22 @@ __device__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, i
 }
 
 // Admit stream position pos (ring slot ri): a z-block (every lane writes its
-// column info, lane 0 the ring entry and the block's clocks) or a bubble.
+// column info -- the tile part is computed once per run -- and lane 0 the
+// ring entry and the block's clocks) or a bubble.
 template <typename R>
 __device__ __forceinline__ void admit(const FsmLaunch &L, const Smem<R> &S, const BcBoxes &bc, int entry, int zh,
-                                      int ri, int clock, int it, int lx, int ly, int lxs, int lys, int rx, int ry)
+                                      int ri, int clock, int it, int lx, int ly, int lxs, int lys, int rx, int ry,
+                                      ColTile &ct)
 {
     u4v ci;
-    int bid = 0, u0flag = 0;
+    int bid = 0;
     if (entry >= 0) {
         const int tz = (entry >> 24) & 0xff;
         bid = tz * L.ntiles + (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
-        u0flag = S.u0ep[bid] != (unsigned short)(it + 1);
-        ci = column_info<R>(L, bc, entry, ri, u0flag, zh, lx, ly, lxs, lys, rx, ry);
+        const int u0flag = S.u0ep[bid] != (unsigned short)(it + 1);
+        if ((entry & 0xffffff) != ct.tile) column_tile<R>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
+        ci.x = ct.col; ci.y = ct.hx; ci.z = ct.hy;
+        ci.w = column_word(L, ct, tz, ri, u0flag, zh);
     } else {
         ci.x = OOB; ci.y = OOB; ci.z = OOB; ci.w = 0;
     }
@@ -883,6 +901,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     R zc, zn, zq;                    // z-upwind values of run starts (vb, vb+1, vb+2)
     float ccv[CCR];
     int ccsize = 0;
+    ColTile ct;
+    ct.tile = -1;
     // prologue decisions: the positions of lane (0,0)'s bricks 0 and 1 (one
     // position, or two when kb = 1); the loop then decides position (B+2)/kb
     int ndecided = 0, nstream = 0x7fffffff, dri = 0;
@@ -894,7 +914,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             nstream = pos;
             break;
         }
-        admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry);
+        admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
         if (SLOWMODE == 2 && e >= 0) {
             cc_issue<CCR>(L, sr, e, ccv, ccsize);
             cc_write<R, CCR>(L, S.cc, dri, ccv, ccsize, (float)L.h);
@@ -954,7 +974,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             if (e == -2) {
                 nstream = pos;
             } else {
-                admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry);
+                admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
                 if (SLOWMODE == 2 && e >= 0) {
                     cc_issue<CCR>(L, sr, e, ccv, ccsize);
                     ccfill = true;
