@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v11"          # bump when the sweep kernel changes; profiles/traffic.json must match
+KERNEL_REV = "fsm-v13"          # bump when the sweep kernel changes; profiles/traffic.json must match
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--chains", type=int, default=0, help="chains per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cores", type=int, default=0)
+    ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -206,7 +207,7 @@ def main():
                        "stations": p.nstat, "events": p.nevents, "parallelism": f"chains sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "fsm_solve_kernel<float, 2, true, 2, 1> (cells via LDS cache, fast sqrt, nrz=4)",
+                         "kernel": "fsm_solve_kernel<float, 2, true, 2, 1, 4> (cells via LDS cache, fast sqrt, nrz=4)",
                          "kernel_rev": KERNEL_REV,
                          "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
                          "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),
@@ -217,6 +218,9 @@ def main():
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
+        if args.raw_stats:
+            line["fsm_raw"] = {"bricks": bricks, "segs": segs, "segs_changed": segs_changed, "iters": iters,
+                               "launches": nlaunch}
         if cpu:
             line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         print(json.dumps(line), flush=True)

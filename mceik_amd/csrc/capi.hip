@@ -143,6 +143,9 @@ static int batch_waves(const FsmLaunch &L, int is_double)
 {
     int per_cu = fsm_occupancy(L, is_double);
     if (per_cu < 1) per_cu = 1;
+    // tuning knob: fewer resident waves per CU (L2 working set experiments)
+    static const int env_cap = [] { const char *e = getenv("MCEIK_WAVES_PER_CU"); return e ? atoi(e) : 0; }();
+    if (env_cap > 0 && env_cap < per_cu) per_cu = env_cap;
     long w = (long)per_cu * device_cus();
     if (w > L.nsolve) w = L.nsolve;
     return (int)(w < 1 ? 1 : w);

@@ -11,6 +11,10 @@
 #define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
 #define MCEIK_KB 4               // bricks per z-block (stream position) when the block tables fit in LDS
 #define MCEIK_MAX_BLOCKS 1024    // per-block clocks in LDS: at most this many z-blocks per field
+#ifndef MCEIK_AHEAD
+#define MCEIK_AHEAD 2            // own segments are loaded this many macro steps ahead (2 or 3;
+                                 // 3 measured 2.8% slower at C3: more visits from the longer in-flight window)
+#endif
 
 // One batched launch: nsolve = nmodel * nstat solves; solve id = model*nstat + station.
 struct FsmLaunch {
@@ -51,8 +55,8 @@ static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 // LDS of one solve wave (byte offsets, shared by host and device):
 //  0 BC boxes [MAX_SRC][6] int | 1 cell cache [nr][ccb] float (cached mode) |
 //  2 diagonal tile order int [ntiles] | 3 lastproc int [nblocks] | 4 lastchg int [nblocks] |
-//  5 u0 epoch u16 [nblocks] | 6 stream entries int [nr] | 7 run scratch int [8] |
-//  8 staged f [8][64] R (uncached) | 9 x halos [8][2][8] R | 10 y halos [8][2][8] R |
+//  5 u0 epoch u16 [nblocks] | 6 stream entries int [nr] + block ids int [nr] | 7 run scratch int [8] |
+//  8 staged f [8][64] R (uncached) | 9+10 halos [32 columns][8] R (two halves of 128 R) |
 //  11 column info [nr][64] uint4
 #define MCEIK_CC_MAX 256         // cell-cache floats per position, upper bound
 #define MCEIK_SMEM_ARRAYS 12
@@ -68,7 +72,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[3] = o; o += mceik_align16(nb * 4);
     off[4] = o; o += mceik_align16(nb * 4);
     off[5] = o; o += mceik_align16(nb * 2);
-    off[6] = o; o += mceik_align16(nr * 4);
+    off[6] = o; o += mceik_align16(nr * 8);
     off[7] = o; o += 32;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 128 * es;
@@ -88,13 +92,16 @@ static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
 // 128-B line per column (32 fp32 / 16 fp64 z values), columns in colpos order.
 // Stream: positions of kb z-bricks (a z-block); kb = 4 when
 // the per-block tables fit, else the smallest power of two that fits (up to
-// the whole column).  Timing rules of the lane pipeline (lag <= 14 steps,
-// loads issued 2 steps ahead, a store is visible to loads issued >= 3 steps
-// later): a visit stays in flight (its changes unknown) for
-// infl = 1 + ceil(16 / kb) positions; an upwind x/y neighbour visit must be
-// >= vis = ceil(12 / kb) positions back; the ring keeps nr = 2 + ceil(16 / kb)
-// positions (the oldest lane reads its position's column info and cells up
-// to kb + 13 steps after the position starts; one position of margin).
+// the whole column).  Timing rules of the lane pipeline (lag <= 14 steps;
+// own segments loaded AHEAD = MCEIK_AHEAD steps ahead, so a position is
+// decided AHEAD steps before lane (0,0) enters it; halos loaded 2 steps ahead; a store is visible to
+// loads issued >= 3 steps later): a visit stays in flight (its changes
+// unknown) for infl = 1 + ceil((14 + AHEAD) / kb) positions (decision at step Q*kb - AHEAD
+// must follow the last lane's last step P*kb + kb - 1 + 14); an upwind x/y
+// neighbour visit must be >= vis = ceil(12 / kb) positions back; the ring
+// keeps nr = 2 + ceil(16 / kb) positions (the oldest lane reads its
+// position's ring entry and cells up to kb + 13 steps after the position
+// starts, the slot is rewritten nr*kb - AHEAD steps after it starts).
 static inline void fsm_geometry(FsmLaunch *L, int es)
 {
     L->ntx = mceik_div_up(L->nx, MCEIK_TILE);
@@ -107,7 +114,7 @@ static inline void fsm_geometry(FsmLaunch *L, int es)
     L->kb = kb;
     L->nzk = mceik_div_up(L->nzb, kb);
     L->nblocks = L->ntiles * L->nzk;
-    L->infl = 1 + mceik_div_up(16, kb);
+    L->infl = 1 + mceik_div_up(14 + MCEIK_AHEAD, kb);
     L->vis = mceik_div_up(12, kb);
     L->nr = 2 + mceik_div_up(16, kb);
     const int bpl = 16 / es;                     // 8-z bricks per 128-B line

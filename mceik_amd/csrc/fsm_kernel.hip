@@ -91,11 +91,15 @@ __device__ __forceinline__ void bload8(Rsrc r, uint32_t off, float (&v)[8])
     f4v b = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
+// cache policy of field stores (experiments: 2 = nt, streaming)
+#ifndef MCEIK_ST_AUX
+#define MCEIK_ST_AUX 0
+#endif
 __device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, const float (&v)[8])
 {
     f4v a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), r, off + 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, MCEIK_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), r, off + 16, 0, MCEIK_ST_AUX);
 }
 __device__ __forceinline__ void bload8(Rsrc r, uint32_t off, double (&v)[8])
 {
@@ -110,7 +114,7 @@ __device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, const double (&v)[
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         d2v a = {v[2 * k], v[2 * k + 1]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off + 16 * k, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off + 16 * k, 0, MCEIK_ST_AUX);
     }
 }
 __device__ __forceinline__ float bload1f(Rsrc r, uint32_t off)
@@ -281,10 +285,12 @@ struct Smem {
     int *order;                  // diagonal tile order: txs | tys << 16   [ntiles]
     int *lastproc, *lastchg;     // per z-block stream clock of the last visit / last visit with a change
     unsigned short *u0ep;        // per z-block iteration+1 of the last u0 store
-    int *ring;                   // per position (mod nr): block entry tx | ty << 12 | tz << 24, bubble -1
+    int *ring;                   // per position (mod nr): block entry tx | ty << 12 | tz << 24, bubble -1;
+                                 // then [nr] the z-block ids
     int *scratch;                // debug counters
     u4v *cinfo;                  // [nr][64] column info of every lane per position
-    R *sf, *shx, *shy;           // staged slowness*h (modes 0,1) and halos
+    R *sf;                       // staged slowness*h (modes 0,1)
+    R *halo;                     // staged halos [32 halo columns][8 z] (halo_col)
 };
 
 template <typename R>
@@ -302,8 +308,7 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     S.ring = reinterpret_cast<int *>(base + off[6]);
     S.scratch = reinterpret_cast<int *>(base + off[7]);
     S.sf = reinterpret_cast<R *>(base + off[8]);
-    S.shx = reinterpret_cast<R *>(base + off[9]);
-    S.shy = reinterpret_cast<R *>(base + off[10]);
+    S.halo = reinterpret_cast<R *>(base + off[9]);     // arrays 9 and 10 are contiguous
     S.cinfo = reinterpret_cast<u4v *>(base + off[11]);
     return S;
 }
@@ -314,18 +319,18 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
 struct Pos {
     int vb, sp, zbs, ri;
 };
-__device__ __forceinline__ void pos_init(Pos &p, int vb, const FsmLaunch &L)
+__device__ __forceinline__ void pos_init(Pos &p, int vb, int kb, int nr)
 {
     p.vb = vb;
     const int v = vb < 0 ? 0 : vb;
-    p.sp = v / L.kb; p.zbs = v - p.sp * L.kb;
-    p.ri = p.sp % L.nr;
+    p.sp = v / kb; p.zbs = v - p.sp * kb;
+    p.ri = p.sp % nr;
 }
-__device__ __forceinline__ void pos_adv(Pos &p, const FsmLaunch &L)
+__device__ __forceinline__ void pos_adv(Pos &p, int kb, int nr)
 {
-    if (p.vb >= 0 && ++p.zbs == L.kb) {
+    if (p.vb >= 0 && ++p.zbs == kb) {
         p.zbs = 0; p.sp++;
-        if (++p.ri == L.nr) p.ri = 0;
+        if (++p.ri == nr) p.ri = 0;
     }
     p.vb++;
 }
@@ -352,6 +357,7 @@ __device__ __forceinline__ int ci_ccb(unsigned w) { return (int)w >> 16; }
 // What a lane needs about one of its bricks.
 struct BInfo {
     uint32_t seg;            // byte offset (u buffer) of the own segment (OOB if none)
+    uint32_t zh;             // the z-upwind node of a run start (prefetch only)
     int zb8, fl, ccb, ri;    // fl: C_* | F_*; ccb: cell-cache index of the brick (SLOWMODE 2); ri: ring slot
     int bid;                 // z-block id (stamps)
     int clk;                 // stream position of the brick (stamps)
@@ -366,9 +372,9 @@ __device__ __forceinline__ void tile_cells(int t, int n, unsigned magic, int &c0
     nc = (int)(((unsigned)b * magic) >> 20) - c0 + 1;
 }
 // Cell range of z-block tz.
-__device__ __forceinline__ void block_zcells(const FsmLaunch &L, int tz, int &cz0, int &ncz)
+__device__ __forceinline__ void block_zcells(const FsmLaunch &L, int kb, int tz, int &cz0, int &ncz)
 {
-    const int a = tz * L.kb * 8, b = min(a + L.kb * 8, L.nz) - 1;
+    const int a = tz * kb * 8, b = min(a + kb * 8, L.nz) - 1;
     cz0 = (int)(((unsigned)a * L.magic_rz) >> 20);
     ncz = (int)(((unsigned)b * L.magic_rz) >> 20) - cz0 + 1;
 }
@@ -423,18 +429,18 @@ __device__ __forceinline__ void column_tile(const FsmLaunch &L, const BcBoxes &b
 }
 // Column info word of block tz of the cached tile at ring slot ri:
 // flags | tz << 8 | cell-cache base << 16, cell of node z = cc[base + z cell].
-__device__ __forceinline__ unsigned column_word(const FsmLaunch &L, const ColTile &t, int tz, int ri, int u0flag,
-                                                int zh)
+__device__ __forceinline__ unsigned column_word(const FsmLaunch &L, int kb, const ColTile &t, int tz, int ri,
+                                                int u0flag, int zh)
 {
     int cz0, nczb;
-    block_zcells(L, tz, cz0, nczb);
+    block_zcells(L, kb, tz, cz0, nczb);
     const int ccb = ri * L.ccb + t.cl * nczb - cz0;
     const int m = t.fl | C_BLK | (u0flag ? C_U0 : 0) | (zh ? C_ZH : 0);
     return (unsigned)(m | (tz << 8) | (ccb << 16));
 }
 
 template <typename R, bool RZ, int ZSH>
-__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
+__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Smem<R> &S, const Pos &p, int nstream,
                                             int lx, int ly, const BcBoxes &bc)
 {
     BInfo b;
@@ -443,13 +449,17 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
     const int e = S.ring[p.ri];
     const unsigned meta = ci.w;
     const int tz = ci_tz(meta);
-    const int zb = tz * L.kb + (RZ ? L.kb - 1 - p.zbs : p.zbs);
+    const int zb = tz * kb + (RZ ? kb - 1 - p.zbs : p.zbs);
     const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < L.nzb;
-    b.seg = valid ? ci.x + zoff_bytes<R>(zb) : OOB;
+    const uint32_t zoff = zoff_bytes<R>(zb);
+    b.seg = valid ? ci.x + zoff : OOB;
+    const int zu = RZ ? zb * 8 + 8 : zb * 8 - 1;             // z-upwind node of the brick's first slot
+    b.zh = (valid && (meta & C_ZH) && p.zbs == 0)
+               ? ci.x + zoff_bytes<R>(zu >> 3) + (uint32_t)(zu & 7) * (uint32_t)sizeof(R) : OOB;
     b.zb8 = valid ? zb * 8 : 0;
     b.ri = p.ri;
     b.clk = p.sp;
-    b.bid = tz * L.ntiles + (e & 0xfff) + ((e >> 12) & 0xfff) * L.ntx;
+    b.bid = S.ring[L.nr + p.ri];                              // z-block id (admit)
     int fl = valid ? (int)((meta & 0x7f) | F_VALID) : 0;
     if (zb == (RZ ? L.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : L.nzb - 1)) fl |= F_LAST;
@@ -479,25 +489,53 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, const Smem<R> &S
     return b;
 }
 
-// Offsets of lane col_lane's segment and halos at stream position p (prefetch),
-// and of its z-upwind node when the brick starts a run inside the column.
-template <typename R, bool RZ>
-__device__ __forceinline__ void seg_offsets(const FsmLaunch &L, const Smem<R> &S, const Pos &p, int nstream,
-                                            uint32_t &seg, uint32_t &hx, uint32_t &hy, uint32_t &zh, int col_lane)
+// Halo columns of a tile (sweep-relative lanes): j = 0..7 the x-upwind halos
+// of lanes (0, j), 8..15 the x-downwind halos of lanes (7, j - 8), 16..23 the
+// y-upwind halos of lanes (j - 16, 0), 24..31 the y-downwind halos of lanes
+// (j - 24, 7).  All 64 lanes load them: lane k fetches half k & 1 (4 z) of
+// column k >> 1's segment for that edge lane's brick vb+2, so one 16-B (fp32)
+// load per lane replaces four 32-B loads of which 48 lanes were idle.
+__device__ __forceinline__ int halo_edge_lane(int j)
 {
-    const u4v ci = S.cinfo[p.ri * 64 + col_lane];
+    return j < 8 ? j * 8 : j < 16 ? (j - 8) * 8 + 7 : j < 24 ? j - 16 : 56 + (j - 24);
+}
+// offset of this lane's half of halo column j at the edge lane's position pe
+template <typename R, bool RZ>
+__device__ __forceinline__ uint32_t halo_offset(const FsmLaunch &L, int kb, const Smem<R> &S, const Pos &pe,
+                                                int nstream, int edge_lane, int j, int half)
+{
+    const u4v ci = S.cinfo[pe.ri * 64 + edge_lane];
     const unsigned meta = ci.w;
-    const int zb = ci_tz(meta) * L.kb + (RZ ? L.kb - 1 - p.zbs : p.zbs);
-    const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < L.nzb;
-    const uint32_t zoff = zoff_bytes<R>(zb);
-    seg = valid ? ci.x + zoff : OOB;
-    hx = valid ? ci.y + zoff : OOB;
-    hy = valid ? ci.z + zoff : OOB;
-    const int zu = RZ ? zb * 8 + 8 : zb * 8 - 1;             // z-upwind node of the brick's first slot
-    zh = (valid && (meta & C_ZH) && p.zbs == 0)
-             ? ci.x + zoff_bytes<R>(zu >> 3) + (uint32_t)(zu & 7) * (uint32_t)sizeof(R) : OOB;
+    const int zb = ci_tz(meta) * kb + (RZ ? kb - 1 - pe.zbs : pe.zbs);
+    const bool valid = pos_valid(pe, nstream) && (meta & C_BLK) && zb < L.nzb;
+    const uint32_t base = j < 16 ? ci.y : ci.z;
+    return valid ? base + zoff_bytes<R>(zb) + (uint32_t)half * 4u * (uint32_t)sizeof(R) : OOB;
+}
+__device__ __forceinline__ void bload4(Rsrc r, uint32_t off, float (&v)[4])
+{
+    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+__device__ __forceinline__ void bload4(Rsrc r, uint32_t off, double (&v)[4])
+{
+    d2v a = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    d2v b = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+template <typename R>
+__device__ __forceinline__ void halo_stage(const Smem<R> &S, int lane, const R (&v)[4])
+{
+    R *d = S.halo + lane * 4;            // = [j][half * 4 + i]
+#pragma unroll
+    for (int i = 0; i < 4; i++) d[i] = v[i];
 }
 
+// Loads / stores that most lanes skip (z-upwind nodes of run starts, u0
+// copies, unchanged segments) are issued only when some lane needs them:
+// every wave-instruction costs address-unit time for all 64 lanes.
+#ifndef MCEIK_SKIP_IDLE_VMEM
+#define MCEIK_SKIP_IDLE_VMEM 1
+#endif
 __device__ __forceinline__ float bload1(Rsrc r, uint32_t off, float)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
@@ -549,14 +587,14 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R> 
 // k - nr) has no reader left.  fp32 entries hold f = s*h (the product the
 // update uses, rounded once as before); fp64 entries hold s.
 template <int CCR>
-__device__ __forceinline__ void cc_issue(const FsmLaunch &L, Rsrc sr, int entry, float (&v)[CCR], int &size)
+__device__ __forceinline__ void cc_issue(const FsmLaunch &L, int kb, Rsrc sr, int entry, float (&v)[CCR], int &size)
 {
     const int lane = threadIdx.x;
     const int tx = entry & 0xfff, ty = (entry >> 12) & 0xfff, tz = (entry >> 24) & 0xff;
     int cx0, ncxt, cy0, ncyt, cz0, nczb;
     tile_cells(tx, L.nx, L.magic_rx, cx0, ncxt);
     tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
-    block_zcells(L, tz, cz0, nczb);
+    block_zcells(L, kb, tz, cz0, nczb);
     size = entry >= 0 ? ncxt * ncyt * nczb : 0;
 #pragma unroll
     for (int r = 0; r < CCR; r++) {
@@ -602,7 +640,7 @@ __device__ __forceinline__ int wave_max(int v)
 // value.  Once a run starts, the next block's z-upwind neighbour is in flight,
 // so the run covers the rest of the column.
 template <typename R, bool RZ>
-__device__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, int rx, int ry, int &zh)
+__device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, int rx, int ry, int &zh)
 {
     const int lane = threadIdx.x;
     const int nt = L.ntiles, nzk = L.nzk;
@@ -668,6 +706,23 @@ __device__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, i
     const int kz = st.k;
     zh = kz == st.k0 && kz > 0;
     const int tz = RZ ? nzk - 1 - kz : kz;
+#ifdef MCEIK_STEPSTATS
+    if (kz > st.k0 && lane == 0) {           // experiment: continuation block clean except its z-upwind
+        const int tx = st.tile & 0xfff, ty = st.tile >> 12, id = ty * L.ntx + tx, b = tz * nt + id;
+        const int txs = rx ? L.ntx - 1 - tx : tx, tys = ry ? L.nty - 1 - ty : ty;
+        const int lp = S.lastproc[b];
+        bool d = S.lastchg[b] >= lp;
+        if (tx > 0) d |= S.lastchg[b - 1] > lp;
+        if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
+        if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
+        if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
+        const int zdn = RZ ? tz - 1 : tz + 1;
+        if (zdn >= 0 && zdn < nzk) d |= S.lastchg[zdn * nt + id] > lp;
+        if (txs > 0) d |= S.lastproc[b + (rx ? 1 : -1)] > C - L.infl;
+        if (tys > 0) d |= S.lastproc[b + (ry ? L.ntx : -L.ntx)] > C - L.infl;
+        if (!d) S.scratch[2]++;
+    }
+#endif
     const int e = st.tile | (tz << 24);
     if (++st.k == nzk) st.tile = -1;
     return e;
@@ -675,32 +730,41 @@ __device__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, i
 
 // Admit stream position pos (ring slot ri): a z-block (every lane writes its
 // column info -- the tile part is computed once per run -- and lane 0 the
-// ring entry and the block's clocks) or a bubble.
+// ring entry, the block id and the block's clocks) or a bubble.  Visit
+// statistics: the bricks lane (0,0) will update (= z-bricks of the block in
+// the grid) and the column segments of all lanes (S.scratch[0], [1]).
 template <typename R>
-__device__ __forceinline__ void admit(const FsmLaunch &L, const Smem<R> &S, const BcBoxes &bc, int entry, int zh,
-                                      int ri, int clock, int it, int lx, int ly, int lxs, int lys, int rx, int ry,
-                                      ColTile &ct)
+__device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> &S, const BcBoxes &bc, int entry,
+                                      int zh, int ri, int clock, int it, int lx, int ly, int lxs, int lys, int rx,
+                                      int ry, ColTile &ct)
 {
     u4v ci;
-    int bid = 0;
+    int bid = 0, nbv = 0;
     if (entry >= 0) {
         const int tz = (entry >> 24) & 0xff;
         bid = tz * L.ntiles + (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
+        nbv = min(kb, L.nzb - tz * kb);
         const int u0flag = S.u0ep[bid] != (unsigned short)(it + 1);
         if ((entry & 0xffffff) != ct.tile) column_tile<R>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         ci.x = ct.col; ci.y = ct.hx; ci.z = ct.hy;
-        ci.w = column_word(L, ct, tz, ri, u0flag, zh);
+        ci.w = column_word(L, kb, ct, tz, ri, u0flag, zh);
     } else {
         ci.x = OOB; ci.y = OOB; ci.z = OOB; ci.w = 0;
     }
+    const int nact = L.visit_stats && entry >= 0 ? __builtin_popcountll(__ballot(ct.fl & C_ACT)) : 0;
     asm volatile("" ::: "memory");
     S.cinfo[ri * 64 + threadIdx.x] = ci;
     if (threadIdx.x == 0) {
         if (entry >= 0) {
             S.u0ep[bid] = (unsigned short)(it + 1);
             S.lastproc[bid] = clock;
+            if (L.visit_stats) {
+                S.scratch[0] += nbv;
+                S.scratch[1] += nbv * nact;
+            }
         }
         S.ring[ri] = entry;
+        S.ring[L.nr + ri] = bid;
     }
     asm volatile("" ::: "memory");
 }
@@ -766,7 +830,6 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
                                           bool xp, bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3;
-    const int hxsel = lxs == 7, hysel = lys >= 4;
     const R self = c[pj];
     const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
     const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
@@ -783,8 +846,8 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
     } else {
         fv = S.sf[pj * 64 + lane];
     }
-    R hxv = S.shx[(pj * 2 + hxsel) * 8 + lys];
-    R hyv = S.shy[(pj * 2 + hysel) * 8 + lxs];
+    R hxv = S.halo[((lxs == 7 ? 8 : 0) + lys) * 8 + pj];
+    R hyv = S.halo[((lys == 7 ? 24 : 16) + lxs) * 8 + pj];
     // keep the LDS reads unconditional (hipcc otherwise sinks them into
     // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
     asm volatile("" : "+v"(hxv), "+v"(hyv));
@@ -880,33 +943,38 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
 // One Gauss-Seidel sweep over the grid in direction (rx, ry, RZ): only the
 // z-blocks admitted by decide() are visited.  Returns the number of stream
 // positions used (z-blocks and bubbles).
-template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR>
+// KB > 0: the launch's kb (bricks per z-block) as a compile-time constant
+// (the ring then has nr = 2 + 16 / KB slots); 0: runtime L.kb / L.nr.
+// nchg: per-lane count of changed column segments (visit statistics).
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
                                      const Smem<R> &S, int rx, int ry, int it, int clock0,
-                                     bool &notconv, int &ierr_last, unsigned long long &visited,
-                                     unsigned long long &segs, unsigned long long &segs_changed)
+                                     bool &notconv, int &ierr_last, unsigned &nchg)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
     const R hr = (R)L.h;
-    const int kb = L.kb;
+    const int kb = KB > 0 ? KB : L.kb;
+    const int nr = KB > 0 ? 2 + (16 + KB - 1) / KB : L.nr;
 
-    const int hxsel = lxs == 7, hysel = lys >= 4;
+    // halo loader role of this lane (halo_edge_lane)
+    const int hj = lane >> 1, hh = lane & 1, he = halo_edge_lane(hj), hd = (he & 7) + (he >> 3);
 
     // stream bookkeeping (wave-uniform)
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
-    R c[8], n[8], q[8], r[8], fq[8], hxq[8], hyq[8], hxn[8], hyn[8];
-    R zc, zn, zq;                    // z-upwind values of run starts (vb, vb+1, vb+2)
+    R c[8], n[8], q[8], p[8], r[8], fq[8], hq[4], hn[4];
+    R zc, zn, zq, zp;                // z-upwind values of run starts (vb .. vb+3)
     float ccv[CCR];
     int ccsize = 0;
     ColTile ct;
     ct.tile = -1;
-    // prologue decisions: the positions of lane (0,0)'s bricks 0 and 1 (one
-    // position, or two when kb = 1); the loop then decides position (B+2)/kb
+    // prologue decisions: the positions of lane (0,0)'s bricks 0..2; the loop
+    // then decides position (B+3)/kb (own segments are loaded 3 steps ahead)
     int ndecided = 0, nstream = 0x7fffffff, dri = 0;
-    for (int pos = 0; pos <= (kb == 1 ? 1 : 0); pos++) {
+    constexpr int AH = MCEIK_AHEAD;      // own segments loaded AH steps ahead (2 or 3)
+    for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
         int zh;
         const int e = decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
         if (e == -2) {
@@ -914,55 +982,53 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             nstream = pos;
             break;
         }
-        admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
+        admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
         if (SLOWMODE == 2 && e >= 0) {
-            cc_issue<CCR>(L, sr, e, ccv, ccsize);
+            cc_issue<CCR>(L, kb, sr, e, ccv, ccsize);
             cc_write<R, CCR>(L, S.cc, dri, ccv, ccsize, (float)L.h);
         }
         ndecided = pos + 1;
-        if (++dri == L.nr) dri = 0;
+        if (++dri == nr) dri = 0;
     }
     asm volatile("" ::: "memory");
-    Pos p1;
-    pos_init(p1, -d, L);
-    BInfo b0 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
-    // prologue: c = brick(vb0), n = brick(vb0+1); stage f and halos of vb0
+    // Brick info of vb (b0), vb+1 (b1), vb+2 (b2); the loop computes vb+3's
+    // (b3) once, uses its offsets for the own-segment prefetch, its halo
+    // offsets one step later, and carries it (one column-info read and decode
+    // per brick).  Own segments are loaded 3 steps ahead, halos 2.
+    Pos p3;
+    pos_init(p3, -d, kb, nr);
+    BInfo b0 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+    // prologue: c, n, q = bricks vb0 .. vb0+2; stage f and halos of vb0
     bload8(ur, b0.seg, c);
     if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
-    {
-        uint32_t s_, hx_, hy_, zh_;
-        seg_offsets<R, RZ>(L, S, p1, nstream, s_, hx_, hy_, zh_, lane);
-        bload8(ur, hx_, hxq);
-        bload8(ur, hy_, hyq);
-        zc = bload1(ur, zh_, R());
-    }
-    pos_adv(p1, L);
-    {
-        uint32_t s1, hx_, hy_, zh_;
-        seg_offsets<R, RZ>(L, S, p1, nstream, s1, hx_, hy_, zh_, lane);
-        bload8(ur, s1, n);
-        bload8(ur, hx_, hxn);            // halos of vb+1: one more step in flight
-        bload8(ur, hy_, hyn);
-        zn = bload1(ur, zh_, R());
+    Pos pe;                              // the halo's edge lane position (vb+2 in the loop)
+    pos_init(pe, -hd, kb, nr);
+    bload4(ur, halo_offset<R, RZ>(L, kb, S, pe, nstream, he, hj, hh), hq);
+    zc = bload1(ur, b0.zh, R());
+    pos_adv(p3, kb, nr);
+    BInfo b1 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+    bload8(ur, b1.seg, n);
+    pos_adv(pe, kb, nr);
+    bload4(ur, halo_offset<R, RZ>(L, kb, S, pe, nstream, he, hj, hh), hn);   // halos of vb+1
+    zn = bload1(ur, b1.zh, R());
+    BInfo b2;
+    if (AH == 3) {
+        pos_adv(p3, kb, nr);
+        b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+        bload8(ur, b2.seg, q);
+        zq = bload1(ur, b2.zh, R());
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         r[i] = UN;
         if (SLOWMODE != 2) S.sf[i * 64 + lane] = fq[i] * hr;
     }
-    if (lxs == 0 || lxs == 7) {
+    halo_stage<R>(S, lane, hq);
 #pragma unroll
-        for (int i = 0; i < 8; i++) S.shx[(i * 2 + hxsel) * 8 + lys] = hxq[i];
-    }
-    if (lys == 0 || lys == 7) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) S.shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) { hxq[i] = hxn[i]; hyq[i] = hyn[i]; }
+    for (int i = 0; i < 4; i++) hq[i] = hn[i];
     asm volatile("" ::: "memory");
 
-    int ph = 2 % kb;                 // (B + 2) mod kb: 0 when lane (0,0)'s vb+2 starts a new position
+    int ph = AH % kb;                // (B + AH) mod kb: 0 when lane (0,0)'s vb+AH starts a new position
     for (int B = 0;; B++) {
         // ---- stream decision for the position lane (0,0) prefetches next
         bool ccfill = false;
@@ -974,30 +1040,30 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             if (e == -2) {
                 nstream = pos;
             } else {
-                admit<R>(L, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
+                admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
                 if (SLOWMODE == 2 && e >= 0) {
-                    cc_issue<CCR>(L, sr, e, ccv, ccsize);
+                    cc_issue<CCR>(L, kb, sr, e, ccv, ccsize);
                     ccfill = true;
                     ccri = dri;
                 }
                 ndecided = pos + 1;
-                if (++dri == L.nr) dri = 0;
+                if (++dri == nr) dri = 0;
             }
         }
         if (nstream != 0x7fffffff && B >= nstream * kb + 14) break;
-        // ---- prefetch: own segment and halos of vb+2 (halos are staged at
-        // the end of the next step: two steps of latency cover), slowness of vb+1
-        const BInfo b1 = brick_info<R, RZ, ZSH>(L, S, p1, nstream, lx, ly, bc);
-        {
-            Pos p2 = p1;
-            pos_adv(p2, L);
-            uint32_t s2, hx_, hy_, zh_;
-            seg_offsets<R, RZ>(L, S, p2, nstream, s2, hx_, hy_, zh_, lane);
-            bload8(ur, s2, q);
-            bload8(ur, hx_, hxn);
-            bload8(ur, hy_, hyn);
-            zq = bload1(ur, zh_, R());
+        // ---- prefetch: own segment of vb+3, halos of vb+2 (staged at the end
+        // of the next step: two steps of latency cover), slowness of vb+1
+        pos_adv(p3, kb, nr);
+        const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+        if (AH == 3) {
+            bload8(ur, b3.seg, p);
+            zp = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
+        } else {
+            bload8(ur, b3.seg, q);
+            zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
         }
+        pos_adv(pe, kb, nr);
+        bload4(ur, halo_offset<R, RZ>(L, kb, S, pe, nstream, he, hj, hh), hn);
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
 
         // ---- the 8 z-slots of the current brick
@@ -1011,17 +1077,14 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         const bool val = (b0.fl & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
-        visited += (unsigned)__builtin_amdgcn_readfirstlane(val ? 1 : 0);   // bricks (lane (0,0) sees each once)
-        if (L.visit_stats) {                                // wave-uniform; SALU popcounts
-            segs += __builtin_popcountll(__ballot(val && (b0.fl & C_ACT)));
-            segs_changed += __builtin_popcountll(__ballot(changed));
-        }
+        nchg += changed ? 1u : 0u;
 
         // ---- write-back, u0 at a block's first visit of the iteration, change stamps
-        bstore8(ur, changed ? b0.seg : OOB, r);
+        if (!MCEIK_SKIP_IDLE_VMEM || __any(changed)) bstore8(ur, changed ? b0.seg : OOB, r);
         {
             R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
-            bstore8(u0r, (m < (R)L.conv_thresh && (b0.fl & C_U0)) ? b0.seg : OOB, c);
+            const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
+            if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
         }
         if (changed) S.lastchg[b0.bid] = clock0 + b0.clk;   // lanes of one block write the same value
         asm volatile("" ::: "memory");
@@ -1032,20 +1095,21 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #pragma unroll
             for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
         }
-        if (lxs == 0 || lxs == 7) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) S.shx[(i * 2 + hxsel) * 8 + lys] = hxq[i];
-        }
-        if (lys == 0 || lys == 7) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) S.shy[(i * 2 + hysel) * 8 + lxs] = hyq[i];
-        }
+        halo_stage<R>(S, lane, hq);
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; hxq[i] = hxn[i]; hyq[i] = hyn[i]; }
+        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; if (AH == 3) q[i] = p[i]; }
+#pragma unroll
+        for (int i = 0; i < 4; i++) hq[i] = hn[i];
         zc = zn; zn = zq;
+        if (AH == 3) zq = zp;
         b0 = b1;
-        pos_adv(p1, L);
+        if (AH == 3) {
+            b1 = b2;
+            b2 = b3;
+        } else {
+            b1 = b3;
+        }
         if (++ph == kb) ph = 0;
     }
     return nstream;
@@ -1186,15 +1250,20 @@ __device__ void build_order(const FsmLaunch &L, int *order)
     }
 }
 
-template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR>
-__global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
+// MCEIK_WPE (experiments): register budget for that many waves per SIMD
+#ifdef MCEIK_WPE
+#define FSM_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE, MCEIK_WPE)))
+#else
+#define FSM_WPE
+#endif
+template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
+__global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Smem<R> S = smem_bind<R>(L, smem);
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
     build_order(L, S.order);
-    unsigned long long visited = 0, segs = 0, segs_changed = 0;
     int pass = 0;
     for (;;) {
         const int snext = next_solve(L, pass);
@@ -1225,6 +1294,8 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
             S.lastproc[t] = -2; S.lastchg[t] = -3;
             S.u0ep[t] = 0;
         }
+        if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
+        unsigned nchg = 0;
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
@@ -1246,16 +1317,29 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
                 const int clock_it = clock;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
+#ifdef MCEIK_STEPSTATS
+                    const int clock_sw = clock;
+#endif
                     // positions used + a gap of infl: the previous sweep's visits are
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
-                        clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last,
-                                              visited, segs, segs_changed);
+                        clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR, KB>(
+                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last, nchg);
                     else
-                        clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last,
-                                              visited, segs, segs_changed);
+                        clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR, KB>(
+                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last, nchg);
+#ifdef MCEIK_STEPSTATS
+                    {   // experiment: visited blocks of this sweep that did not change
+                        const int c1 = clock - L.infl;
+                        unsigned nu = 0;
+                        for (int t = lane; t < L.nblocks; t += 64) {
+                            const int lp = S.lastproc[t];
+                            nu += (lp >= c1 - 0x100000 && lp > 63 && lp >= clock_sw && S.lastchg[t] < lp) ? 1u : 0u;
+                        }
+                        for (int o = 32; o > 0; o >>= 1) nu += __shfl_xor(nu, o, 64);
+                        if (lane == 0) S.scratch[3] += nu;
+                    }
+#endif
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 }
@@ -1270,6 +1354,20 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
         int ierr = ierr_last;
         for (int o = 32; o > 0; o >>= 1) ierr = max(ierr, __shfl_xor(ierr, o, 64));
         if (!ok) ierr = 1;
+        if (L.visit_stats) {
+            for (int o = 32; o > 0; o >>= 1) nchg += __shfl_xor(nchg, o, 64);
+            asm volatile("" ::: "memory");
+            if (lane == 0) {
+                atomicAdd(L.visit_stats, (unsigned long long)(unsigned)S.scratch[0]);
+#ifdef MCEIK_STEPSTATS
+                atomicAdd(L.visit_stats + 1, (unsigned long long)(unsigned)S.scratch[2]);
+                atomicAdd(L.visit_stats + 2, (unsigned long long)(unsigned)S.scratch[3]);
+#else
+                atomicAdd(L.visit_stats + 1, (unsigned long long)(unsigned)S.scratch[1]);
+                atomicAdd(L.visit_stats + 2, (unsigned long long)nchg);
+#endif
+            }
+        }
         if (lane == 0) {
             if (L.iter_total) atomicAdd(L.iter_total, (unsigned long long)iters);
             if (L.niter) L.niter[solve] = iters;
@@ -1285,11 +1383,6 @@ __global__ __launch_bounds__(64) void fsm_solve_kernel(FsmLaunch L)
         }
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    }
-    if (lane == 0 && L.visit_stats) {
-        atomicAdd(L.visit_stats, visited);
-        atomicAdd(L.visit_stats + 1, segs);
-        atomicAdd(L.visit_stats + 2, segs_changed);
     }
 }
 
@@ -1331,19 +1424,19 @@ __global__ void from_brick_kernel(const RS *src, RD *dst, FsmLaunch L, int nfiel
 }  // namespace
 
 // ---- host-side launchers (C++ linkage, used by capi.hip) ---------------------
-template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR>
+template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 static hipError_t launch_fsm(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     size_t lds = fsm_lds_bytes(L, sizeof(R));
-    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR>), dim3(nwaves), dim3(64), lds, st, L);
+    hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR, KB>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
 }
 
-template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR>
+template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 static int occupancy_of(size_t lds)
 {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR>, 64,
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR, KB>, 64,
                                                         lds) == hipSuccess ? nb : 1;
 }
 
@@ -1353,25 +1446,26 @@ static int occupancy_of(size_t lds)
 static int variant(const FsmLaunch &L, int is_double)
 {
     const int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
-    if (is_double) return 8 + mode * 2;
+    if (is_double) return 9 + mode * 2;
     if (mode != 2) return mode * 2;
-    return 4 + (L.fast_sqrt ? 1 : 0) + (L.nrz == 4 && L.fast_sqrt && L.ccb <= 64 ? 2 : 0);
+    return 4 + (L.fast_sqrt ? 1 : 0) + (L.nrz == 4 && L.fast_sqrt && L.ccb <= 64 ? (L.kb == MCEIK_KB ? 3 : 2) : 0);
 }
 
 #define FSM_VARIANTS(X)                         \
-    X(0, float, 0, false, -1, 1)                \
-    X(2, float, 1, false, -1, 1)                \
-    X(4, float, 2, false, -1, 4)                \
-    X(5, float, 2, true, -1, 4)                 \
-    X(7, float, 2, true, 2, 1)                  \
-    X(8, double, 0, false, -1, 1)               \
-    X(10, double, 1, false, -1, 1)              \
-    X(12, double, 2, false, -1, 4)
+    X(0, float, 0, false, -1, 1, 0)             \
+    X(2, float, 1, false, -1, 1, 0)             \
+    X(4, float, 2, false, -1, 4, 0)             \
+    X(5, float, 2, true, -1, 4, 0)              \
+    X(7, float, 2, true, 2, 1, 0)               \
+    X(8, float, 2, true, 2, 1, MCEIK_KB)        \
+    X(9, double, 0, false, -1, 1, 0)            \
+    X(11, double, 1, false, -1, 1, 0)           \
+    X(13, double, 2, false, -1, 4, 0)
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st)
 {
     switch (variant(L, is_double)) {
-#define X(v, R, M, F, Z, CR) case v: return launch_fsm<R, M, F, Z, CR>(L, nwaves, st);
+#define X(v, R, M, F, Z, CR, K) case v: return launch_fsm<R, M, F, Z, CR, K>(L, nwaves, st);
         FSM_VARIANTS(X)
 #undef X
     default: return hipErrorInvalidValue;
@@ -1382,7 +1476,7 @@ int fsm_occupancy(const FsmLaunch &L, int is_double)
 {
     const size_t lds = fsm_lds_bytes(L, is_double ? 8 : 4);
     switch (variant(L, is_double)) {
-#define X(v, R, M, F, Z, CR) case v: return occupancy_of<R, M, F, Z, CR>(lds);
+#define X(v, R, M, F, Z, CR, K) case v: return occupancy_of<R, M, F, Z, CR, K>(lds);
         FSM_VARIANTS(X)
 #undef X
     default: return 1;

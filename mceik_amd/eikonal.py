@@ -143,8 +143,11 @@ class BatchSolver:
     """
 
     def __init__(self, nx, ny, nz, h, x0=0.0, y0=0.0, z0=0.0, maxit=50, tol=1e-8, precision=32,
-                 nref=None):
+                 nref=None, fast_sqrt=False):
         self.nx, self.ny, self.nz, self.h = int(nx), int(ny), int(nz), float(h)
+        # fast_sqrt (cells mode): the caller guarantees f = h * slowness >= 1e-12 (a
+        # normal float), as the sampler does from vmax; results are unchanged
+        self.fast_sqrt = bool(fast_sqrt)
         self.x0, self.y0, self.z0 = float(x0), float(y0), float(z0)
         self.maxit, self.tol, self.precision = int(maxit), float(tol), int(precision)
         self.nref = nref
@@ -161,6 +164,7 @@ class BatchSolver:
         b.nrx, b.nry, b.nrz = nr
         b.nev = nev
         b.max_sweeps = max_sweeps
+        b.fast_sqrt = 1 if (self.fast_sqrt and slow_mode == 1) else 0
         return b
 
     def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None):

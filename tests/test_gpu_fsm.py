@@ -119,10 +119,14 @@ def test_fp32_batch_many_models_and_stations():
             assert int(out["niter"][k]) == it
 
 
-def test_fp32_inversion_grid_mode_bitwise():
-    """slow_mode 1: per-cell slowness (nref refinement) == twin on the expanded field."""
+@pytest.mark.parametrize("fast,nz", [(False, 34), (True, 34), (True, 20), (True, 67)],
+                         ids=["exact_sqrt_kb4", "fast_kb4", "fast_kb3", "fast_kb4_ragged"])
+def test_fp32_inversion_grid_mode_bitwise(fast, nz):
+    """slow_mode 1: per-cell slowness (nref refinement) == twin on the expanded field.
+    fast=True runs the sampler's kernel (LDS cell cache, short sqrt); nz >= 25
+    gives 4-brick z-blocks (the compile-time-kb variant used at 128^3)."""
     dev = _dev()
-    nx, ny, nz, h, nref = 30, 26, 34, 100.0, (4, 4, 4)
+    nx, ny, h, nref = 30, 26, 100.0, (4, 4, 4)
     ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
     rng = np.random.default_rng(9)
     v = rng.integers(2500, 6500, (ncz, ncy, ncx)).astype(np.int32)
@@ -130,7 +134,8 @@ def test_fp32_inversion_grid_mode_bitwise():
     k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
     sfield = scell[k // nref[2], j // nref[1], i // nref[0]].ravel()
     src = np.array([[[0.0, 1234.5, 987.6, (nz - 1) * h]], [[0.0, 300.0, 2200.0, (nz - 1) * h]]])
-    bs = _solver(nx, ny, nz, h, 32, nref=nref)
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=fast)
     out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(1, -1), device=dev), want_fields=True)
     u = out["u"].cpu().numpy().reshape(2, -1)
     for s in range(2):

@@ -40,10 +40,12 @@ def test_initial_loglik_matches_oracle():
     s.close()
 
 
-def test_accept_sequence_bit_identical():
+@pytest.mark.parametrize("n", [24, 40], ids=["n24_kb3", "n40_kb4"])
+def test_accept_sequence_bit_identical(n):
+    """n = 40 runs 4-brick z-blocks: the compile-time-kb kernel of the 128^3 bench."""
     _dev()
     from mceik_amd import mcmc
-    p = _problem()
+    p = _problem(n=n)
     nch, nsteps, off = 4, 6, 11
     s = mcmc.Sampler(p, nchains=nch, chain_offset=off)
     v0, logl0, _, _ = s.state()
