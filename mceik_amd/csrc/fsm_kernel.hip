@@ -536,6 +536,60 @@ __device__ __forceinline__ void halo_stage(const Smem<R> &S, int lane, const R (
 #ifndef MCEIK_SKIP_IDLE_VMEM
 #define MCEIK_SKIP_IDLE_VMEM 1
 #endif
+// Pair-coalesced segment loads (fp32; MCEIK_PAIR_LOAD): lanes 2i and 2i+1
+// read the two 16-B halves of lane 2i's segment with one instruction and of
+// lane 2i+1's with the other, so each wave-instruction touches 32 lines
+// instead of 64; pair_finish() swaps the halves into place (DPP quad_perm
+// [1,0,3,2]) once the data has arrived.
+#ifndef MCEIK_PAIR_LOAD
+#define MCEIK_PAIR_LOAD 1
+#endif
+__device__ __forceinline__ unsigned dpp_swap_pair(unsigned v)
+{
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void pair_issue(Rsrc r, uint32_t seg, float (&a)[4], float (&b)[4])
+{
+    const bool odd = threadIdx.x & 1;
+    const uint32_t segp = dpp_swap_pair(seg);
+    bload4(r, odd ? segp + 16u : seg, a);       // even: own [0,4)  odd: partner's [4,8)
+    bload4(r, odd ? seg + 16u : segp, b);       // even: partner's [0,4)  odd: own [4,8)
+}
+__device__ __forceinline__ void pair_finish(const float (&a)[4], const float (&b)[4], float (&v)[8])
+{
+    const bool odd = threadIdx.x & 1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float send = odd ? a[i] : b[i];
+        const float recv = __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(unsigned, send)));
+        v[i] = odd ? recv : a[i];
+        v[4 + i] = odd ? b[i] : recv;
+    }
+}
+
+// Pair-coalesced segment store (fp32): the same pairing for the write-back of
+// changed segments (each instruction stores the two halves of one lane's
+// segment, predicated on that lane's change).
+__device__ __forceinline__ void bstore4(Rsrc r, uint32_t off, float a0, float a1, float a2, float a3)
+{
+    f4v a = {a0, a1, a2, a3};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, MCEIK_ST_AUX);
+}
+__device__ __forceinline__ void pair_store(Rsrc r, uint32_t seg, bool chg, const float (&v)[8])
+{
+    const bool odd = threadIdx.x & 1;
+    const uint32_t own = chg ? seg : OOB;
+    const uint32_t oth = dpp_swap_pair(own);    // partner's offset (OOB if unchanged)
+    float x[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        x[i] = __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(unsigned, odd ? v[i] : v[4 + i])));
+    // even: own [0,4) | odd: even's [4,8)         even: odd's [0,4) | odd: own [4,8)
+    // (branch-free selects: both instructions carry all 64 lanes)
+    bstore4(r, odd ? oth + 16u : own, odd ? x[0] : v[0], odd ? x[1] : v[1], odd ? x[2] : v[2], odd ? x[3] : v[3]);
+    bstore4(r, odd ? own + 16u : oth, odd ? v[4] : x[0], odd ? v[5] : x[1], odd ? v[6] : x[2], odd ? v[7] : x[3]);
+}
+
 __device__ __forceinline__ float bload1(Rsrc r, uint32_t off, float)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
@@ -965,6 +1019,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     R c[8], n[8], q[8], p[8], r[8], fq[8], hq[4], hn[4];
+    constexpr bool PAIR = MCEIK_PAIR_LOAD && sizeof(R) == 4 && MCEIK_AHEAD == 2;
+    float qa[4], qb[4];                  // PAIR: raw halves of q
     R zc, zn, zq, zp;                // z-upwind values of run starts (vb .. vb+3)
     float ccv[CCR];
     int ccsize = 0;
@@ -1059,7 +1115,10 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             bload8(ur, b3.seg, p);
             zp = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
         } else {
-            bload8(ur, b3.seg, q);
+            if (PAIR)
+                pair_issue(ur, b3.seg, qa, qb);
+            else
+                bload8(ur, b3.seg, q);
             zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
         }
         pos_adv(pe, kb, nr);
@@ -1080,7 +1139,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         nchg += changed ? 1u : 0u;
 
         // ---- write-back, u0 at a block's first visit of the iteration, change stamps
-        if (!MCEIK_SKIP_IDLE_VMEM || __any(changed)) bstore8(ur, changed ? b0.seg : OOB, r);
+        if (!MCEIK_SKIP_IDLE_VMEM || __any(changed)) {
+            if (PAIR)
+                pair_store(ur, b0.seg, changed, reinterpret_cast<const float (&)[8]>(r));
+            else
+                bstore8(ur, changed ? b0.seg : OOB, r);
+        }
         {
             R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
             const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
@@ -1098,7 +1162,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         halo_stage<R>(S, lane, hq);
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < 8; i++) { c[i] = n[i]; n[i] = q[i]; if (AH == 3) q[i] = p[i]; }
+        for (int i = 0; i < 8; i++) {
+            c[i] = n[i];
+            if (!PAIR) n[i] = q[i];
+            if (AH == 3) q[i] = p[i];
+        }
+        if (PAIR) pair_finish(qa, qb, reinterpret_cast<float (&)[8]>(n));
 #pragma unroll
         for (int i = 0; i < 4; i++) hq[i] = hn[i];
         zc = zn; zn = zq;
