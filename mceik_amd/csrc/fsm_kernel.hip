@@ -875,18 +875,48 @@ __device__ __forceinline__ double godunov_v(double a, double b, double c, double
     return godunov(a, b, c, f, e);
 }
 
+// Halo values of a brick (MCEIK_HALO_VEC): the lane's x-halo and y-halo rows
+// (8 z each, only tile-edge lanes use them) read with 16-B LDS loads before
+// the slot loop -- 4 ds_read_b128 per brick instead of 16 ds_read_b32.
+#ifndef MCEIK_HALO_VEC
+#define MCEIK_HALO_VEC 1
+#endif
+// MCEIK_BPERM_EARLY: the brick's 16 y-neighbour ds_bpermutes issued before the
+// slot loop (brick_update) instead of one pair per slot
+#ifndef MCEIK_BPERM_EARLY
+#define MCEIK_BPERM_EARLY 1
+#endif
+__device__ __forceinline__ void lds_row8(const float *p, float (&v)[8])
+{
+    const f4v a = reinterpret_cast<const f4v *>(p)[0], b = reinterpret_cast<const f4v *>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void lds_row8(const double *p, double (&v)[8])
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const d2v a = reinterpret_cast<const d2v *>(p)[k];
+        v[2 * k] = a.x; v[2 * k + 1] = a.y;
+    }
+}
+
 // x/y neighbour minima and f = s*h of slot pj.  The x and y neighbours come
 // from the other lanes' r (updated in their previous step) and n, which the
 // current step does not modify, so any slot may gather them at any time.
 template <typename R, int SLOWMODE, int ZSH, bool GENERIC, bool WANTF>
 __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, const R (&c)[8],
-                                          const R (&n)[8], const R (&r)[8], int pj, int aup, int adn,
-                                          bool xp, bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
+                                          const R (&n)[8], const R (&r)[8], const R (&hx)[8], const R (&hy)[8],
+                                          const R (&ymv)[8], const R (&ypvv)[8], int pj, int aup, int adn, bool xp,
+                                          bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3;
     const R self = c[pj];
     const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
+#if MCEIK_BPERM_EARLY
+    const R ym = ymv[pj], ypv = ypvv[pj];
+#else
     const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
+#endif
     if (!WANTF) {
     } else if (SLOWMODE == 2) {
         if (ZSH >= 0 && !GENERIC) {
@@ -900,11 +930,15 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
     } else {
         fv = S.sf[pj * 64 + lane];
     }
+#if MCEIK_HALO_VEC
+    const R hxv = hx[pj], hyv = hy[pj];
+#else
     R hxv = S.halo[((lxs == 7 ? 8 : 0) + lys) * 8 + pj];
     R hyv = S.halo[((lys == 7 ? 24 : 16) + lxs) * 8 + pj];
     // keep the LDS reads unconditional (hipcc otherwise sinks them into
     // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
     asm volatile("" : "+v"(hxv), "+v"(hyv));
+#endif
     R xup = lxs > 0 ? xm : hxv;
     R xdn = lxs < 7 ? xpv : hxv;
     R yup = lys > 0 ? ym : hyv;
@@ -943,6 +977,23 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
     const R zprev = (fl & F_ZH) ? zc : r[RZ ? 0 : 7];
     int aup = ((lane - 8) & 63) * 4, adn = ((lane + 8) & 63) * 4;
     asm volatile("" : "+v"(aup), "+v"(adn));
+    R hx[8], hy[8], ymv[8], ypvv[8];
+    if (MCEIK_HALO_VEC) {
+        const int lxs = lane & 7, lys = lane >> 3;
+        lds_row8(S.halo + ((lxs == 7 ? 8 : 0) + lys) * 8, hx);
+        lds_row8(S.halo + ((lys == 7 ? 24 : 16) + lxs) * 8, hy);
+    }
+    if (MCEIK_BPERM_EARLY) {
+        // all y-neighbour exchanges of the brick up front (r holds the previous
+        // step's values until slot j overwrites r[pj], n is not written): the
+        // LDS latency then overlaps the z chain instead of stalling each slot
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            ymv[i] = bperm(aup, r[i]);
+            ypvv[i] = bperm(adn, n[i]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
     // fast fp32 path over the LDS cell cache: f, f*f, 2f*f per cell
     constexpr bool CELLF = SLOWMODE == 2 && ZSH >= 0 && !GENERIC && sizeof(R) == 4;
     R fc = 0, ffc = 0, ff2c = 0;
@@ -953,7 +1004,8 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
         const int pnext = RZ ? pj - 1 : pj + 1;
         const R self = c[pj];
         R ux, uy, fv;
-        gather_xy<R, SLOWMODE, ZSH, GENERIC, !CELLF>(L, S, b0, c, n, r, pj, aup, adn, xp, xn, yp, yn, ux, uy, fv);
+        gather_xy<R, SLOWMODE, ZSH, GENERIC, !CELLF>(L, S, b0, c, n, r, hx, hy, ymv, ypvv, pj, aup, adn, xp, xn, yp,
+                                                     yn, ux, uy, fv);
         if (CELLF) {
             // one LDS read and one f*f per slowness cell (2^ZSH slots)
             if (j == 0 || (pj >> (ZSH < 0 ? 0 : ZSH)) != (pprev >> (ZSH < 0 ? 0 : ZSH))) {
@@ -1084,8 +1136,18 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     for (int i = 0; i < 4; i++) hq[i] = hn[i];
     asm volatile("" ::: "memory");
 
+#ifndef MCEIK_ROTATE
+#define MCEIK_ROTATE 0               // 1: two steps per loop iteration with swapped roles (measured 0.5% slower at C3)
+#endif
     int ph = AH % kb;                // (B + AH) mod kb: 0 when lane (0,0)'s vb+AH starts a new position
-    for (int B = 0;; B++) {
+    int B = 0;
+    // One macro step.  The rotating buffers come in their roles of this step
+    // (c: the brick being updated, n: the next one, hq: halos staged at the
+    // end of the step, hn: halos loaded in it); the loop below alternates the
+    // roles, so no buffer is copied between steps: the brick after next lands
+    // in c's registers, which the next step passes as its n.  Returns false at
+    // the end of the stream.
+    auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
         // ---- stream decision for the position lane (0,0) prefetches next
         bool ccfill = false;
         int ccri = 0;
@@ -1106,7 +1168,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (++dri == nr) dri = 0;
             }
         }
-        if (nstream != 0x7fffffff && B >= nstream * kb + 14) break;
+        if (nstream != 0x7fffffff && B >= nstream * kb + 14) return false;
         // ---- prefetch: own segment of vb+3, halos of vb+2 (staged at the end
         // of the next step: two steps of latency cover), slowness of vb+1
         pos_adv(p3, kb, nr);
@@ -1161,15 +1223,16 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
         halo_stage<R>(S, lane, hq);
         asm volatile("" ::: "memory");
+        // ---- rotation: the brick after next into c's registers (the next step's n)
+        if (PAIR) {
+            pair_finish(qa, qb, reinterpret_cast<float (&)[8]>(c));
+        } else {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            c[i] = n[i];
-            if (!PAIR) n[i] = q[i];
-            if (AH == 3) q[i] = p[i];
+            for (int i = 0; i < 8; i++) {
+                c[i] = q[i];
+                if (AH == 3) q[i] = p[i];
+            }
         }
-        if (PAIR) pair_finish(qa, qb, reinterpret_cast<float (&)[8]>(n));
-#pragma unroll
-        for (int i = 0; i < 4; i++) hq[i] = hn[i];
         zc = zn; zn = zq;
         if (AH == 3) zq = zp;
         b0 = b1;
@@ -1180,6 +1243,32 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             b1 = b3;
         }
         if (++ph == kb) ph = 0;
+        B++;
+        return true;
+    };
+    if (KB > 0 && MCEIK_ROTATE) {
+        // the hot (compile-time kb) variant: two steps per iteration, roles swapped
+        for (;;) {
+            if (!step(c, n, hq, hn)) break;
+            if (!step(n, c, hn, hq)) break;
+        }
+    } else {
+        // runtime-kb variants stay one step per iteration (unrolled, they spill)
+        for (;;) {
+            if (!step(c, n, hq, hn)) break;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const R t = c[i];
+                c[i] = n[i];
+                n[i] = t;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const R t = hq[i];
+                hq[i] = hn[i];
+                hn[i] = t;
+            }
+        }
     }
     return nstream;
 }
