@@ -1136,18 +1136,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     for (int i = 0; i < 4; i++) hq[i] = hn[i];
     asm volatile("" ::: "memory");
 
-#ifndef MCEIK_ROTATE
-#define MCEIK_ROTATE 0               // 1: two steps per loop iteration with swapped roles (measured 0.5% slower at C3)
-#endif
     int ph = AH % kb;                // (B + AH) mod kb: 0 when lane (0,0)'s vb+AH starts a new position
-    int B = 0;
-    // One macro step.  The rotating buffers come in their roles of this step
-    // (c: the brick being updated, n: the next one, hq: halos staged at the
-    // end of the step, hn: halos loaded in it); the loop below alternates the
-    // roles, so no buffer is copied between steps: the brick after next lands
-    // in c's registers, which the next step passes as its n.  Returns false at
-    // the end of the stream.
-    auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
+    for (int B = 0;; B++) {
         // ---- stream decision for the position lane (0,0) prefetches next
         bool ccfill = false;
         int ccri = 0;
@@ -1168,7 +1158,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (++dri == nr) dri = 0;
             }
         }
-        if (nstream != 0x7fffffff && B >= nstream * kb + 14) return false;
+        if (nstream != 0x7fffffff && B >= nstream * kb + 14) break;
         // ---- prefetch: own segment of vb+3, halos of vb+2 (staged at the end
         // of the next step: two steps of latency cover), slowness of vb+1
         pos_adv(p3, kb, nr);
@@ -1200,6 +1190,41 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         notconv |= nc && val;
         nchg += changed ? 1u : 0u;
 
+        // ---- consume this step's loads before any store of the step is issued.
+        // gfx9's vmcnt retires loads and stores in issue order, so a wait for a
+        // load placed after the write-back (the loop's register copies of the
+        // prefetched values) would also wait for those stores to complete.
+        // Stage the prefetched slowness/halos of vb+1 for the next step (the
+        // update has read this step's halos), finish the brick after next and
+        // rotate the z-upwind and halo registers.
+        if (SLOWMODE == 2) {
+            if (ccfill) cc_write<R, CCR>(L, S.cc, ccri, ccv, ccsize, (float)L.h);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
+        }
+        halo_stage<R>(S, lane, hq);
+        R nn[8];
+        if (PAIR) {
+            pair_finish(qa, qb, reinterpret_cast<float (&)[8]>(nn));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                nn[i] = q[i];
+                if (AH == 3) q[i] = p[i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) hq[i] = hn[i];
+        zc = zn; zn = zq;
+        if (AH == 3) zq = zp;
+        // materialise the copies here (the loads' waits land here, before the
+        // stores); otherwise they become the loop's phi copies at the latch
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("" : "+v"(nn[i]));
+        asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]), "+v"(zn));
+        asm volatile("" ::: "memory");
+
         // ---- write-back, u0 at a block's first visit of the iteration, change stamps
         if (!MCEIK_SKIP_IDLE_VMEM || __any(changed)) {
             if (PAIR)
@@ -1214,27 +1239,11 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
         if (changed) S.lastchg[b0.bid] = clock0 + b0.clk;   // lanes of one block write the same value
         asm volatile("" ::: "memory");
-        // ---- stage the prefetched slowness/halos of vb+1 for the next step
-        if (SLOWMODE == 2) {
-            if (ccfill) cc_write<R, CCR>(L, S.cc, ccri, ccv, ccsize, (float)L.h);
-        } else {
 #pragma unroll
-            for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
+        for (int i = 0; i < 8; i++) {
+            c[i] = n[i];
+            n[i] = nn[i];
         }
-        halo_stage<R>(S, lane, hq);
-        asm volatile("" ::: "memory");
-        // ---- rotation: the brick after next into c's registers (the next step's n)
-        if (PAIR) {
-            pair_finish(qa, qb, reinterpret_cast<float (&)[8]>(c));
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                c[i] = q[i];
-                if (AH == 3) q[i] = p[i];
-            }
-        }
-        zc = zn; zn = zq;
-        if (AH == 3) zq = zp;
         b0 = b1;
         if (AH == 3) {
             b1 = b2;
@@ -1243,32 +1252,6 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             b1 = b3;
         }
         if (++ph == kb) ph = 0;
-        B++;
-        return true;
-    };
-    if (KB > 0 && MCEIK_ROTATE) {
-        // the hot (compile-time kb) variant: two steps per iteration, roles swapped
-        for (;;) {
-            if (!step(c, n, hq, hn)) break;
-            if (!step(n, c, hn, hq)) break;
-        }
-    } else {
-        // runtime-kb variants stay one step per iteration (unrolled, they spill)
-        for (;;) {
-            if (!step(c, n, hq, hn)) break;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const R t = c[i];
-                c[i] = n[i];
-                n[i] = t;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const R t = hq[i];
-                hq[i] = hn[i];
-                hn[i] = t;
-            }
-        }
     }
     return nstream;
 }
