@@ -446,7 +446,6 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Sm
     BInfo b;
     const int lane = threadIdx.x;
     const u4v ci = S.cinfo[p.ri * 64 + lane];
-    const int e = S.ring[p.ri];
     const unsigned meta = ci.w;
     const int tz = ci_tz(meta);
     const int zb = tz * kb + (RZ ? kb - 1 - p.zbs : p.zbs);
@@ -468,6 +467,7 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Sm
     b.bcm = 0;
     if (__any(fl & C_BC)) {
         // BC z-slots of this column segment (rare: columns through a source box)
+        const int e = S.ring[p.ri];
         const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
         unsigned m = 0;
         if (fl & C_BC) {
@@ -650,11 +650,15 @@ __device__ __forceinline__ void cc_issue(const FsmLaunch &L, int kb, Rsrc sr, in
     tile_cells(ty, L.ny, L.magic_ry, cy0, ncyt);
     block_zcells(L, kb, tz, cz0, nczb);
     size = entry >= 0 ? ncxt * ncyt * nczb : 0;
+    // small exact divisions (idx < 64 * CCR <= 256, divisors <= 256): the
+    // quotient of (a + 1/2) / d is >= 1/512 away from an integer, far above
+    // the error of v_rcp_f32 and one rounding, so truncation gives floor(a / d)
+    const float rz = __builtin_amdgcn_rcpf((float)nczb), rx = __builtin_amdgcn_rcpf((float)ncxt);
 #pragma unroll
     for (int r = 0; r < CCR; r++) {
         const int idx = lane + 64 * r;
-        const int cz = idx % nczb, t = idx / nczb;
-        const int cyl = t / ncxt, cxl = t - cyl * ncxt;
+        const int t = (int)(((float)idx + 0.5f) * rz), cz = idx - t * nczb;
+        const int cyl = (int)(((float)t + 0.5f) * rx), cxl = t - cyl * ncxt;
         const uint32_t off = (uint32_t)((((cz0 + cz) * L.ncy + cy0 + cyl) * L.ncx) + cx0 + cxl) * 4u;
         v[r] = bload1f(sr, idx < size ? off : OOB);
     }
@@ -1137,7 +1141,16 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     asm volatile("" ::: "memory");
 
     int ph = AH % kb;                // (B + AH) mod kb: 0 when lane (0,0)'s vb+AH starts a new position
-    for (int B = 0;; B++) {
+    // MCEIK_ROTATE (compile-time kb only): two steps per loop iteration with
+    // the roles of the brick (c/n) and halo (hq/hn) registers swapped, so
+    // neither is copied between steps and a halo load is first waited for
+    // when it is staged, one step after it was issued
+#ifndef MCEIK_ROTATE
+#define MCEIK_ROTATE 0       // measured 1% slower at C3 (v17), kept as an option
+#endif
+    constexpr bool ROT = MCEIK_ROTATE && KB > 0;
+    int B = 0;
+    auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
         // ---- stream decision for the position lane (0,0) prefetches next
         bool ccfill = false;
         int ccri = 0;
@@ -1158,7 +1171,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (++dri == nr) dri = 0;
             }
         }
-        if (nstream != 0x7fffffff && B >= nstream * kb + 14) break;
+        if (nstream != 0x7fffffff && B >= nstream * kb + 14) return false;
         // ---- prefetch: own segment of vb+3, halos of vb+2 (staged at the end
         // of the next step: two steps of latency cover), slowness of vb+1
         pos_adv(p3, kb, nr);
@@ -1214,15 +1227,18 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (AH == 3) q[i] = p[i];
             }
         }
+        if (!ROT) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) hq[i] = hn[i];
+            for (int i = 0; i < 4; i++) hq[i] = hn[i];
+        }
         zc = zn; zn = zq;
         if (AH == 3) zq = zp;
         // materialise the copies here (the loads' waits land here, before the
         // stores); otherwise they become the loop's phi copies at the latch
 #pragma unroll
         for (int i = 0; i < 8; i++) asm volatile("" : "+v"(nn[i]));
-        asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]), "+v"(zn));
+        if (!ROT) asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]));
+        asm volatile("" : "+v"(zn));
         asm volatile("" ::: "memory");
 
         // ---- write-back, u0 at a block's first visit of the iteration, change stamps
@@ -1241,8 +1257,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            c[i] = n[i];
-            n[i] = nn[i];
+            if (ROT) {
+                c[i] = nn[i];            // c's registers become the next step's n
+            } else {
+                c[i] = n[i];
+                n[i] = nn[i];
+            }
         }
         b0 = b1;
         if (AH == 3) {
@@ -1252,6 +1272,17 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             b1 = b3;
         }
         if (++ph == kb) ph = 0;
+        B++;
+        return true;
+    };
+    if (ROT) {
+        for (;;) {
+            if (!step(c, n, hq, hn)) break;
+            if (!step(n, c, hn, hq)) break;
+        }
+    } else {
+        while (step(c, n, hq, hn)) {
+        }
     }
     return nstream;
 }
