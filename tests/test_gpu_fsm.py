@@ -144,6 +144,30 @@ def test_fp32_inversion_grid_mode_bitwise(fast, nz):
         assert int(out["niter"][s]) == it
 
 
+def test_fp32_inversion_grid_mode_8brick_blocks():
+    """136 x 136 x 128: 17 x 17 tiles x 16 z-bricks would be 1156 four-brick
+    z-blocks, more than the LDS block tables hold (MCEIK_MAX_BLOCKS = 1024), so
+    the stream runs 8-brick blocks -- the runtime-kb kernel that the 256^3
+    configuration (C5) uses.  Bitwise == twin on the expanded field."""
+    dev = _dev()
+    nx = ny = 136
+    nz, h, nref = 128, 100.0, (4, 4, 4)
+    ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
+    rng = np.random.default_rng(11)
+    v = rng.integers(2500, 6500, (ncz, ncy, ncx)).astype(np.int32)
+    scell = (1.0 / v.astype(np.float32)).astype(np.float32)
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    sfield = scell[k // nref[2], j // nref[1], i // nref[0]].ravel()
+    src = np.array([[[0.0, 6543.2, 7012.3, (nz - 1) * h]]])
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=True)
+    out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(1, -1), device=dev), want_fields=True)
+    u = out["u"].cpu().numpy().reshape(1, -1)
+    t, _, it = O.eikonal_solve(nx, ny, nz, sfield, h, src[0], dtype=np.float32)
+    assert np.array_equal(u[0].view(np.uint32), t.view(np.uint32))
+    assert int(out["niter"][0]) == it
+
+
 FSM_FILES = sorted(glob.glob(os.path.join(GOLD, "fsm_*.npz")))
 
 
