@@ -328,10 +328,13 @@ __device__ __forceinline__ void pos_init(Pos &p, int vb, int kb, int nr)
 }
 __device__ __forceinline__ void pos_adv(Pos &p, int kb, int nr)
 {
-    if (p.vb >= 0 && ++p.zbs == kb) {
-        p.zbs = 0; p.sp++;
-        if (++p.ri == nr) p.ri = 0;
-    }
+    // branch-free (lanes differ in vb): selects instead of exec-mask branches
+    const int z1 = p.zbs + (p.vb >= 0 ? 1 : 0);
+    const bool wrap = z1 == kb;
+    const int r1 = p.ri + (wrap ? 1 : 0);
+    p.zbs = wrap ? 0 : z1;
+    p.sp += wrap ? 1 : 0;
+    p.ri = r1 == nr ? 0 : r1;
     p.vb++;
 }
 __device__ __forceinline__ bool pos_valid(const Pos &p, int nstream)
@@ -441,11 +444,9 @@ __device__ __forceinline__ unsigned column_word(const FsmLaunch &L, int kb, cons
 
 template <typename R, bool RZ, int ZSH>
 __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Smem<R> &S, const Pos &p, int nstream,
-                                            int lx, int ly, const BcBoxes &bc)
+                                            int lx, int ly, const BcBoxes &bc, const u4v ci)
 {
     BInfo b;
-    const int lane = threadIdx.x;
-    const u4v ci = S.cinfo[p.ri * 64 + lane];
     const unsigned meta = ci.w;
     const int tz = ci_tz(meta);
     const int zb = tz * kb + (RZ ? kb - 1 - p.zbs : p.zbs);
@@ -501,10 +502,9 @@ __device__ __forceinline__ int halo_edge_lane(int j)
 }
 // offset of this lane's half of halo column j at the edge lane's position pe
 template <typename R, bool RZ>
-__device__ __forceinline__ uint32_t halo_offset(const FsmLaunch &L, int kb, const Smem<R> &S, const Pos &pe,
-                                                int nstream, int edge_lane, int j, int half)
+__device__ __forceinline__ uint32_t halo_offset(const FsmLaunch &L, int kb, const Pos &pe, int nstream, int j,
+                                                int half, const u4v ci)     // ci: the edge lane's column info at pe
 {
-    const u4v ci = S.cinfo[pe.ri * 64 + edge_lane];
     const unsigned meta = ci.w;
     const int zb = ci_tz(meta) * kb + (RZ ? kb - 1 - pe.zbs : pe.zbs);
     const bool valid = pos_valid(pe, nstream) && (meta & C_BLK) && zb < L.nzb;
@@ -1109,24 +1109,24 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     // per brick).  Own segments are loaded 3 steps ahead, halos 2.
     Pos p3;
     pos_init(p3, -d, kb, nr);
-    BInfo b0 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+    BInfo b0 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
     // prologue: c, n, q = bricks vb0 .. vb0+2; stage f and halos of vb0
     bload8(ur, b0.seg, c);
     if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
     Pos pe;                              // the halo's edge lane position (vb+2 in the loop)
     pos_init(pe, -hd, kb, nr);
-    bload4(ur, halo_offset<R, RZ>(L, kb, S, pe, nstream, he, hj, hh), hq);
+    bload4(ur, halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]), hq);
     zc = bload1(ur, b0.zh, R());
     pos_adv(p3, kb, nr);
-    BInfo b1 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+    BInfo b1 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
     bload8(ur, b1.seg, n);
     pos_adv(pe, kb, nr);
-    bload4(ur, halo_offset<R, RZ>(L, kb, S, pe, nstream, he, hj, hh), hn);   // halos of vb+1
+    bload4(ur, halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]), hn);   // halos of vb+1
     zn = bload1(ur, b1.zh, R());
     BInfo b2;
     if (AH == 3) {
         pos_adv(p3, kb, nr);
-        b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+        b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
         bload8(ur, b2.seg, q);
         zq = bload1(ur, b2.zh, R());
     }
@@ -1174,8 +1174,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (nstream != 0x7fffffff && B >= nstream * kb + 14) return false;
         // ---- prefetch: own segment of vb+3, halos of vb+2 (staged at the end
         // of the next step: two steps of latency cover), slowness of vb+1
+        // (both column-info reads issued before either is decoded: one LDS
+        // latency per step instead of two)
         pos_adv(p3, kb, nr);
-        const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc);
+        pos_adv(pe, kb, nr);
+        const u4v ci3 = S.cinfo[p3.ri * 64 + lane], cie = S.cinfo[pe.ri * 64 + he];
+        const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, ci3);
         if (AH == 3) {
             bload8(ur, b3.seg, p);
             zp = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
@@ -1186,8 +1190,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 bload8(ur, b3.seg, q);
             zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
         }
-        pos_adv(pe, kb, nr);
-        bload4(ur, halo_offset<R, RZ>(L, kb, S, pe, nstream, he, hj, hh), hn);
+        bload4(ur, halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, cie), hn);
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
 
         // ---- the 8 z-slots of the current brick
