@@ -759,6 +759,9 @@ __device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R> &S, Stre
     }
     if (st.wait > 0) {
         st.wait--;
+#ifdef MCEIK_BUBBLESTATS
+        if (threadIdx.x == 0) S.scratch[3]++;          // experiment: bubble positions
+#endif
         return -1;
     }
     const int kz = st.k;
@@ -1539,7 +1542,11 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                 atomicAdd(L.visit_stats + 2, (unsigned long long)(unsigned)S.scratch[3]);
 #else
                 atomicAdd(L.visit_stats + 1, (unsigned long long)(unsigned)S.scratch[1]);
+#ifdef MCEIK_BUBBLESTATS
+                atomicAdd(L.visit_stats + 2, (unsigned long long)(unsigned)S.scratch[3]);
+#else
                 atomicAdd(L.visit_stats + 2, (unsigned long long)nchg);
+#endif
 #endif
             }
         }
