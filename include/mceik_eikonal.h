@@ -95,6 +95,10 @@ typedef struct mceik_fsm_batch {
     unsigned long long *visit_stats; /* device [3] += brick visits (8x8x8 nodes, one sweep; z-blocks
                                         whose inputs did not change are skipped), column segments
                                         (8 nodes) updated, segments that changed; or NULL */
+    const int *solve_order;     /* device [nmodel*nstat]: work-queue slot -> solve id (a permutation;
+                                   only the order solves start in changes), or NULL = model-major */
+    unsigned long long *solve_clock; /* device [nmodel*nstat][2]: s_memrealtime (100 MHz) at the
+                                        start and end of each solve (diagnostic), or NULL */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */

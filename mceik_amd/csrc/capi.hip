@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/mceik.h"
@@ -102,6 +103,8 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.niter = b->niter; L.ierr = b->ierr;
     L.iter_total = b->iter_total;
     L.visit_stats = b->visit_stats;
+    L.solve_order = b->solve_order;
+    L.solve_clock = b->solve_clock;
 }
 
 static int g_device_cus = 0;
@@ -680,10 +683,40 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         mceik_mcmc_finalize(&s);
         return -1;
     }
-    // initial log-likelihood of every chain
+    // initial log-likelihood of every chain.  MCEIK_SOLVE_CLOCK_REPORT=1: time
+    // every solve of this launch and print how busy the persistent waves were
+    // (diagnostic for the work-queue tail)
+    unsigned long long *d_clock = nullptr;
+    const char *rep_env = getenv("MCEIK_SOLVE_CLOCK_REPORT");
+    const bool report = rep_env && rep_env[0] == '1';
+    if (report && dalloc(s, &d_clock, (size_t)nch * nstat * 2)) {
+        mceik_mcmc_finalize(&s);
+        return -1;
+    }
+    b.solve_clock = d_clock;
     if (mcmc_forward(s, false) || mcmc_init_loglik(D, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
         mceik_mcmc_finalize(&s);
         return -1;
+    }
+    b.solve_clock = nullptr;
+    if (report) {
+        std::vector<unsigned long long> clk((size_t)nch * nstat * 2);
+        if (hipMemcpy(clk.data(), d_clock, clk.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            unsigned long long t0 = ~0ull, t1 = 0;
+            double busy = 0.0, dmin = 1e30, dmax = 0.0;
+            for (size_t i = 0; i < clk.size(); i += 2) {
+                t0 = clk[i] < t0 ? clk[i] : t0;
+                t1 = clk[i + 1] > t1 ? clk[i + 1] : t1;
+                const double d = (double)(clk[i + 1] - clk[i]);
+                busy += d;
+                dmin = d < dmin ? d : dmin;
+                dmax = d > dmax ? d : dmax;
+            }
+            const int nw = ws_layout(&b).nwaves;
+            fprintf(stderr, "mceik solve clock: %d solves on %d waves, launch %.1f ms, solve %.1f..%.1f ms "
+                            "(mean %.1f), waves busy %.2f%%\n", nch * nstat, nw, (t1 - t0) * 1e-5, dmin * 1e-5,
+                    dmax * 1e-5, busy / (nch * nstat) * 1e-5, 100.0 * busy / ((double)nw * (double)(t1 - t0)));
+        }
     }
     hipMemset(s->d_iters, 0, 4 * sizeof(unsigned long long));
     *out = s;

@@ -48,6 +48,8 @@ struct FsmLaunch {
     unsigned *counter;           // 8 work-queue heads, 128 B apart (zeroed before the launch)
     unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
     unsigned long long *visit_stats;  // [3] += tile visits, column-segment updates, changed segments; may be null
+    const int *solve_order;      // queue slot -> solve id, or null (slot = solve)
+    unsigned long long *solve_clock;  // [nsolve][2] realtime at solve start / end, or null
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }

@@ -1408,7 +1408,7 @@ __device__ __forceinline__ int next_solve(const FsmLaunch &L, int &pass)
         unsigned i = 0;
         if (threadIdx.x == 0) i = atomicAdd(L.counter + 32 * g, 1u);
         i = __builtin_amdgcn_readfirstlane(__shfl(i, 0, 64));
-        if ((int)i < hi - lo) return lo + (int)i;
+        if ((int)i < hi - lo) return L.solve_order ? L.solve_order[lo + (int)i] : lo + (int)i;
         pass++;
     }
     return -1;
@@ -1447,6 +1447,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         const int snext = next_solve(L, pass);
         if (snext < 0) break;
         const unsigned solve = (unsigned)snext;
+        if (L.solve_clock && lane == 0) L.solve_clock[2 * (size_t)solve] = __builtin_amdgcn_s_memrealtime();
         const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
         const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
         R *u = reinterpret_cast<R *>(L.u) + slot * L.field_elems;
@@ -1551,6 +1552,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             }
         }
         if (lane == 0) {
+            if (L.solve_clock) L.solve_clock[2 * (size_t)solve + 1] = __builtin_amdgcn_s_memrealtime();
             if (L.iter_total) atomicAdd(L.iter_total, (unsigned long long)iters);
             if (L.niter) L.niter[solve] = iters;
             if (L.ierr) L.ierr[solve] = ierr;

@@ -167,7 +167,12 @@ class BatchSolver:
         b.fast_sqrt = 1 if (self.fast_sqrt and slow_mode == 1) else 0
         return b
 
-    def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None):
+    def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None,
+              solve_order=None, solve_clock=False):
+        """solve_order: optional permutation of the nmodel*nstat solve ids (the
+        order the work queues hand them out; results do not depend on it).
+        solve_clock: also return out["clock"] [nsolve][2], the device realtime
+        (100 MHz) at the start and end of every solve."""
         import torch
         dev = slow.device
         sources = sources.to(device=dev, dtype=torch.float64).contiguous()
@@ -189,6 +194,17 @@ class BatchSolver:
         b.src = sources.data_ptr()
         b.slow = slow.data_ptr()
         b.niter, b.ierr = niter.data_ptr(), ierr.data_ptr()
+        if solve_order is not None:
+            solve_order = torch.as_tensor(solve_order, dtype=torch.int32).to(dev).contiguous()
+            if solve_order.numel() != nsolve or not torch.equal(torch.sort(solve_order.cpu())[0],
+                                                                torch.arange(nsolve, dtype=torch.int32)):
+                raise ValueError("solve_order must be a permutation of the solve ids")
+            b.solve_order = solve_order.data_ptr()
+            out["_order"] = solve_order
+        if solve_clock:
+            clock = torch.zeros((nsolve, 2), dtype=torch.int64, device=dev)
+            b.solve_clock = clock.data_ptr()
+            out["clock"] = clock
         if nev:
             ev_node = ev_node.to(device=dev, dtype=torch.int32).contiguous()
             ttab = torch.empty((nsolve, nev), dtype=torch.float32, device=dev)

@@ -144,6 +144,31 @@ def test_fp32_inversion_grid_mode_bitwise(fast, nz):
         assert int(out["niter"][s]) == it
 
 
+def test_solve_order_and_clock():
+    """A permuted work order (mceik_fsm_batch.solve_order) gives bitwise the
+    same fields, tables and iteration counts; solve_clock stamps every solve."""
+    dev = _dev()
+    nx, ny, nz, h = 20, 18, 22, 100.0
+    rng = np.random.default_rng(5)
+    nmodel, nstat = 3, 4
+    slows = np.stack([(1.0 / _rough(nx, ny, nz, 20 + m)).ravel().astype(np.float32) for m in range(nmodel)])
+    src = np.stack([np.array([[0.0, rng.uniform(0, 1900), rng.uniform(0, 1700), rng.uniform(0, 2100)]])
+                    for _ in range(nstat)])
+    ev = torch.tensor(rng.integers(0, nx * ny * nz, 5).astype(np.int32))
+    sl = torch.tensor(slows.reshape(nmodel, nz, ny, nx), device=dev)
+    bs = _solver(nx, ny, nz, h, 32)
+    a = bs.solve(torch.tensor(src), sl, ev_node=ev, want_fields=True)
+    perm = rng.permutation(nmodel * nstat).astype(np.int32)
+    b = bs.solve(torch.tensor(src), sl, ev_node=ev, want_fields=True, solve_order=perm, solve_clock=True)
+    assert torch.equal(a["u"].view(torch.int32), b["u"].view(torch.int32))
+    assert torch.equal(a["ttab"].view(torch.int32), b["ttab"].view(torch.int32))
+    assert torch.equal(a["niter"], b["niter"])
+    clk = b["clock"].cpu().numpy()
+    assert (clk[:, 0] > 0).all() and (clk[:, 1] >= clk[:, 0]).all()
+    with pytest.raises(ValueError):
+        bs.solve(torch.tensor(src), sl, solve_order=np.zeros(nmodel * nstat, np.int32))
+
+
 def test_fp32_inversion_grid_mode_8brick_blocks():
     """136 x 136 x 128: 17 x 17 tiles x 16 z-bricks would be 1156 four-brick
     z-blocks, more than the LDS block tables hold (MCEIK_MAX_BLOCKS = 1024), so
