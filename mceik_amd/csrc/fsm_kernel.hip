@@ -1141,6 +1141,20 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     halo_stage<R>(S, lane, hq);
 #pragma unroll
     for (int i = 0; i < 4; i++) hq[i] = hn[i];
+    // Wait for the prologue's loads here, once per sweep: a register the loop
+    // carries in from a prologue load would otherwise count as a pending load
+    // at the loop head, and its first use in every step would wait on vmcnt --
+    // i.e. for the previous step's write-back stores as well.
+#pragma unroll
+    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(c[i]), "+v"(n[i]));
+#pragma unroll
+    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(hq[i]));
+    asm volatile("" : "+v"(zc), "+v"(zn));
+    if (AH == 3) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("" : "+v"(q[i]));
+        asm volatile("" : "+v"(zq));
+    }
     asm volatile("" ::: "memory");
 
     int ph = AH % kb;                // (B + AH) mod kb: 0 when lane (0,0)'s vb+AH starts a new position
@@ -1152,6 +1166,10 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #define MCEIK_ROTATE 0       // measured 1% slower at C3 (v17), kept as an option
 #endif
     constexpr bool ROT = MCEIK_ROTATE && KB > 0;
+#ifndef MCEIK_CC_DEFER
+#define MCEIK_CC_DEFER 1
+#endif
+    int cc_pend = -1;                // ring slot whose cell loads (ccv) are written next step
     int B = 0;
     auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
         // ---- stream decision for the position lane (0,0) prefetches next
@@ -1182,6 +1200,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         pos_adv(p3, kb, nr);
         pos_adv(pe, kb, nr);
         const u4v ci3 = S.cinfo[p3.ri * 64 + lane], cie = S.cinfo[pe.ri * 64 + he];
+        __builtin_amdgcn_sched_barrier(0);     // keep the two reads ahead of every use
         const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, ci3);
         if (AH == 3) {
             bload8(ur, b3.seg, p);
@@ -1217,7 +1236,15 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         // update has read this step's halos), finish the brick after next and
         // rotate the z-upwind and halo registers.
         if (SLOWMODE == 2) {
-            if (ccfill) cc_write<R, CCR>(L, S.cc, ccri, ccv, ccsize, (float)L.h);
+            // cells of the position admitted one step earlier: lane (0,0)
+            // enters it at the next step, so a step of latency cover is free
+            // (kb >= 2: the next admission, which reloads ccv, is >= 2 steps on)
+            if (MCEIK_CC_DEFER && kb >= 2) {
+                if (cc_pend >= 0) cc_write<R, CCR>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
+                cc_pend = ccfill ? ccri : -1;
+            } else if (ccfill) {
+                cc_write<R, CCR>(L, S.cc, ccri, ccv, ccsize, (float)L.h);
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
