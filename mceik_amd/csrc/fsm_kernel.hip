@@ -1085,8 +1085,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     int ccsize = 0;
     ColTile ct;
     ct.tile = -1;
-    // prologue decisions: the positions of lane (0,0)'s bricks 0..2; the loop
-    // then decides position (B+3)/kb (own segments are loaded 3 steps ahead)
+    // prologue decisions: the positions of lane (0,0)'s bricks 0..AH-1; the
+    // loop then decides position (B+AH)/kb (own segments are loaded AH steps
+    // ahead, MCEIK_AHEAD = 2)
     int ndecided = 0, nstream = 0x7fffffff, dri = 0;
     constexpr int AH = MCEIK_AHEAD;      // own segments loaded AH steps ahead (2 or 3)
     for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
@@ -1106,10 +1107,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (++dri == nr) dri = 0;
     }
     asm volatile("" ::: "memory");
-    // Brick info of vb (b0), vb+1 (b1), vb+2 (b2); the loop computes vb+3's
-    // (b3) once, uses its offsets for the own-segment prefetch, its halo
-    // offsets one step later, and carries it (one column-info read and decode
-    // per brick).  Own segments are loaded 3 steps ahead, halos 2.
+    // Brick info of vb (b0), vb+1 (b1) [and vb+2 (b2) when AH = 3]; the loop
+    // computes vb+AH's (b3) once, uses its offsets for the own-segment
+    // prefetch and carries it (one column-info read and decode per brick).
     Pos p3;
     pos_init(p3, -d, kb, nr);
     BInfo b0 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
@@ -1193,8 +1193,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             }
         }
         if (nstream != 0x7fffffff && B >= nstream * kb + 14) return false;
-        // ---- prefetch: own segment of vb+3, halos of vb+2 (staged at the end
-        // of the next step: two steps of latency cover), slowness of vb+1
+        // ---- prefetch: own segment and halos of vb+AH (consumed at the end
+        // of this step, before its stores; halos staged to LDS at the end of
+        // the next), slowness of vb+1 (modes 0/1)
         // (both column-info reads issued before either is decoded: one LDS
         // latency per step instead of two)
         pos_adv(p3, kb, nr);
