@@ -89,3 +89,34 @@ def test_ctypes_mirrors_match_header():
     assert C.sizeof(_lib.EikParms) == sizes["eik"]
     assert C.sizeof(_lib.MceikParms) == sizes["parms"]
     assert _lib.MceikParms.nrefz.offset == int(_layout(INC).split("mceik_parms_struct.nrefz ")[1].split()[0])
+
+
+def _offsets_c(header, ctype, fields):
+    """sizeof and offsetof(every field) of a C struct, from gcc on the public header."""
+    body = "".join(f'  printf("{f} %zu\\n", offsetof({ctype}, {f}));\n' for f in fields)
+    src = (f'#include <stdio.h>\n#include <stddef.h>\n#include "{header}"\n'
+           f'int main(void) {{\n  printf("sizeof %zu\\n", sizeof({ctype}));\n{body}  return 0;\n}}\n')
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "o.c")
+        open(p, "w").write(src)
+        exe = os.path.join(td, "o")
+        subprocess.run(["gcc", "-I", INC, p, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    return dict(zip(out[0::2], map(int, out[1::2])))
+
+
+@pytest.mark.parametrize("header,ctype,pyname", [
+    ("mceik_eikonal.h", "mceik_fsm_batch", "FsmBatch"),
+    ("mceik_eikonal.h", "mceik_relocate_batch", "RelocateBatch"),
+    ("mceik.h", "mceik_mcmc_opts", "McmcOpts"),
+])
+def test_ctypes_batch_structs_match_public_headers(header, ctype, pyname):
+    """Every field of the ctypes mirrors sits at the C offset (the batch
+    descriptors are passed by pointer across the C-ABI)."""
+    from mceik_amd import _lib
+    cls = getattr(_lib, pyname)
+    names = [f[0] for f in cls._fields_]
+    c = _offsets_c(header, ctype, names)
+    assert C.sizeof(cls) == c["sizeof"]
+    for n in names:
+        assert getattr(cls, n).offset == c[n], n
