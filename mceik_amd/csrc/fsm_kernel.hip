@@ -1282,7 +1282,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             else
                 bstore8(ur, changed ? b0.seg : OOB, r);
         }
-        {
+        if (!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) {      // a block's first visit in the iteration
             R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
             const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
             if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
