@@ -248,7 +248,11 @@ template <typename R> struct Lay {
 template <typename R>
 __device__ __forceinline__ uint32_t zoff_bytes(int zb)
 {
-    return (uint32_t)(zb / Lay<R>::BPL) * 8192u + (uint32_t)(zb % Lay<R>::BPL) * 8u * (uint32_t)sizeof(R);
+    // shifts, not the (zb / BPL) * (8192 - 128) + zb * 32 the compiler would
+    // otherwise form (v_mul_lo_u32 is quarter rate); zb >= 0 wherever used
+    constexpr int LB = Lay<R>::BPL == 4 ? 2 : 1, LS = sizeof(R) == 4 ? 5 : 6;
+    const uint32_t u = (uint32_t)zb;
+    return ((u >> LB) << 13) | ((u & (uint32_t)(Lay<R>::BPL - 1)) << LS);
 }
 template <typename R>
 __device__ __forceinline__ uint32_t tile_bytes(const FsmLaunch &L) { return (uint32_t)L.nzq * 8192u; }
