@@ -29,10 +29,15 @@ KERNEL_REV = "fsm-v21"          # bump when the sweep kernel changes; profiles/t
 
 
 # ---------------------------------------------------------------- CPU baseline
+CPU_ROUNDS = 5
+
+
 def _ref_solve_worker(args):
-    """One fp64 solve by the REFERENCE's own eikonal3d_serial_driver
-    (oracle/_ref/libfsm3d_ref.so, built from fsm3d.f90); single-threaded."""
-    so, n, h, src, slow_path = args
+    """Single-threaded fp64 solves by the REFERENCE's own eikonal3d_serial_driver
+    (oracle/_ref/libfsm3d_ref.so, built from fsm3d.f90): job 1 (level
+    structure) and one warm-up solve untimed, then `rounds` job-2 solves, each
+    timed alone.  Returns the per-solve seconds."""
+    so, n, h, src, slow_path, rounds = args
     os.environ["OMP_NUM_THREADS"] = "1"
     lib = C.CDLL(so)
     slow = np.load(slow_path)
@@ -45,17 +50,33 @@ def _ref_solve_worker(args):
     args_ = lambda job: (i(job), i(0), i(50), i(1), i(n), i(n), i(n), d(1e-8), d(h), d(0.0), d(0.0), d(0.0),
                          P(ts), P(xs), P(ys), P(zs), P(slow), P(u), C.byref(ierr))
     lib.eikonal3d_serial_driver(*args_(1))
-    t = time.perf_counter()
-    lib.eikonal3d_serial_driver(*args_(2))
-    dt = time.perf_counter() - t
+    lib.eikonal3d_serial_driver(*args_(2))              # warm-up
+    times = []
+    for _ in range(rounds):
+        t = time.perf_counter()
+        lib.eikonal3d_serial_driver(*args_(2))
+        times.append(time.perf_counter() - t)
+        if ierr.value != 0:
+            raise RuntimeError(f"reference solve failed, ierr = {ierr.value}")
     lib.eikonal3d_serial_driver(*args_(3))
-    return dt, ierr.value
+    return times
 
 
-def cpu_baseline(p, v0, cores):
-    """Reference proposals/s on this host: `cores` single-threaded fp64 solves in
-    parallel (the reference's table-parallel design, mpiutils.f90:147-149),
-    proposals/s = solves/s / stations.  Runs before the GPU is initialised."""
+def cpu_cores():
+    """Host cores for the CPU baseline: the CPUs this process may run on,
+    capped by OMP_NUM_THREADS -- the GPU box allots 16 CPUs per GPU while
+    nproc reports the whole machine."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", 0) or 0)
+    return min(avail, cap) if cap > 0 else avail
+
+
+def cpu_baseline(p, v0, cores, rounds=CPU_ROUNDS):
+    """Reference proposals/s on this host (SURVEY s.8d protocol): `cores`
+    single-threaded fp64 solves run concurrently, one per core (the reference's
+    table-parallel design, mpiutils.f90:147-149); per core one warm-up solve,
+    then `rounds` timed job-2 solves.  proposals/s = cores / median solve time
+    / stations.  Runs before the GPU is initialised."""
     import multiprocessing as mp
     import tempfile
     k, j, i = np.meshgrid(np.arange(p.nz), np.arange(p.ny), np.arange(p.nx), indexing="ij")
@@ -63,18 +84,16 @@ def cpu_baseline(p, v0, cores):
     slow = np.ascontiguousarray((1.0 / v0[cell.ravel()].astype(np.float64)))
     srcs = [(0.0, p.sx[s % p.nstat], p.sy[s % p.nstat], p.sz[s % p.nstat]) for s in range(cores)]
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libfsm3d_ref.so")
-    sample = f"{cores} fp64 solves (128^3 model of chain 0, stations 0..{cores - 1}), 1 thread each"
+    nproc = os.cpu_count()
     if os.path.exists(ref_so):
         with tempfile.TemporaryDirectory() as td:
             sp = os.path.join(td, "slow.npy")
             np.save(sp, slow)
             ctx = mp.get_context("spawn")
             with ctx.Pool(cores) as pool:
-                t = time.perf_counter()
-                res = pool.map(_ref_solve_worker, [(ref_so, p.nx, p.h, s, sp) for s in srcs])
-                wall = time.perf_counter() - t
+                res = pool.map(_ref_solve_worker, [(ref_so, p.nx, p.h, s, sp, rounds) for s in srcs])
         kind = "reference"
-        cpu_s = sum(r[0] for r in res)
+        times = np.array(res).ravel()
     else:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import _oracle as O
@@ -82,14 +101,22 @@ def cpu_baseline(p, v0, cores):
         xs = np.array([s[1] for s in srcs]); ys = np.array([s[2] for s in srcs]); zs = np.array([s[3] for s in srcs])
         out = np.zeros(cores)
         idx = np.zeros(cores, np.int32)
-        t = time.perf_counter()
-        L.oracle_batch_solve_f64(cores, 50, p.nx, p.ny, p.nz, 1e-8, p.h, 0.0, 0.0, 0.0, O._p(xs), O._p(ys),
-                                 O._p(zs), O._p(slow), O._p(idx), O._p(out), 0, cores)
-        wall = time.perf_counter() - t
+        times = []
+        for r in range(rounds + 1):
+            t = time.perf_counter()
+            L.oracle_batch_solve_f64(cores, 50, p.nx, p.ny, p.nz, 1e-8, p.h, 0.0, 0.0, 0.0, O._p(xs), O._p(ys),
+                                     O._p(zs), O._p(slow), O._p(idx), O._p(out), 0, cores)
+            if r:
+                times.append(time.perf_counter() - t)     # wall of `cores` concurrent solves
         kind = "port"
-        cpu_s = wall * cores
-    return {"value": round(cores / wall / p.nstat, 5), "unit": "proposals/s", "cores": cores, "kind": kind,
-            "sample": f"{sample}; wall {wall:.2f} s, {cpu_s:.1f} CPU-s; proposals/s = solves/s / {p.nstat} stations"}
+        times = np.array(times)
+    med = float(np.median(times))
+    return {"value": round(cores / med / p.nstat, 5), "unit": "proposals/s", "cores": cores, "kind": kind,
+            "sample": f"{p.nx}^3 fp64 solves of chain 0's model, stations 0..{cores - 1}: {cores} concurrent "
+                      f"single-threaded solves (host nproc {nproc}, {cores} CPUs allotted), 1 warm-up + "
+                      f"{rounds} timed job-2 solves per core; median solve {med:.3f} s, mean "
+                      f"{float(np.mean(times)):.3f} s, min {float(np.min(times)):.3f} s, max "
+                      f"{float(np.max(times)):.3f} s; proposals/s = cores / median / {p.nstat} stations"}
 
 
 # ---------------------------------------------------------------- main
@@ -102,6 +129,8 @@ def main():
     ap.add_argument("--chains", type=int, default=0, help="chains per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cores", type=int, default=0)
+    ap.add_argument("--cpu-rounds", type=int, default=CPU_ROUNDS)
+    ap.add_argument("--sigma", type=float, default=1e-3, help="pick noise (s); varObs = sigma^2")
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     args = ap.parse_args()
 
@@ -120,8 +149,7 @@ def main():
     v0 = mcmc.initial_models(p, range(lo, hi))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cores = args.cpu_cores or int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(p, v0[0], cores)
+        cpu = cpu_baseline(p, v0[0], args.cpu_cores or cpu_cores(), args.cpu_rounds)
 
     import torch
     import torch.distributed as dist
@@ -132,13 +160,15 @@ def main():
     # picks from the GPU forward of the true model (replaces the analytic ones)
     tt = mcmc.picks_from_forward(local_rank)(p)
     rng = np.random.default_rng(p.seed + 1)
-    p.tobs = tt.T.ravel().astype(np.float64) + rng.normal(0.0, 0.05, p.nevents * p.nstat)
+    # pick noise sigma and varObs = sigma^2 at the scale one proposal moves a
+    # travel time (~1 ms for 50 m/s on a 400-m cell), so the posterior is not
+    # flat at the proposal scale and Metropolis both accepts and rejects
+    p.tobs = tt.T.ravel().astype(np.float64) + rng.normal(0.0, args.sigma, p.nevents * p.nstat)
+    p.var[:] = args.sigma ** 2
     p.nburn, p.keepk = args.warmup, max(1, args.steps)
     smp = mcmc.Sampler(p, nchains=hi - lo, chain_offset=lo, v0=v0, max_samples=1, device=local_rank)
     stream = torch.cuda.current_stream(dev)
     smp.set_stream(stream.cuda_stream)
-    post = torch.empty((hi - lo, p.ncell), dtype=torch.int32, device=dev)
-    gathered = ([torch.empty_like(post) for _ in range(world)] if rank == 0 else None) if world > 1 else None
 
     if args.warmup:
         smp.run(args.warmup)
@@ -150,9 +180,11 @@ def main():
     t0 = time.perf_counter()
     smp.run(args.steps)
     # checkpoint: the kept posterior states of every chain -> rank 0 (RCCL over xGMI)
-    smp.samples(max_states=1, device_ptr=post.data_ptr())
     if world > 1:
-        dist.gather(post, gathered, dst=0)
+        post, _ = mcmc.gather_kept(smp, per_gpu * world, device=dev)
+    else:
+        post = torch.empty((hi - lo, p.ncell), dtype=torch.int32, device=dev)
+        smp.samples(max_states=1, device_ptr=post.data_ptr())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -200,7 +232,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY s.8d heterogeneous model, picks = GPU forward of the true model + N(0,0.05 s))",
+            "data": f"synthetic (SURVEY s.8d heterogeneous model, picks = GPU forward of the true model + "
+                    f"N(0, {args.sigma} s), varObs = {args.sigma}^2)",
             "config": {"workload": f"{args.config}: {per_gpu} chains/GPU, {p.nx}^3 grid, {p.nstat} stations, "
                                    f"{p.nevents} events, nref=4",
                        "chains_per_gpu": per_gpu, "chains_total": per_gpu * world, "grid": [p.nx, p.ny, p.nz],

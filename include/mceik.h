@@ -7,8 +7,8 @@
  * passes its rank/size and shards chains.  Every function
  * returns 0 on success (h5io.c convention).
  */
-#ifndef MCEIK_H_AMD
-#define MCEIK_H_AMD 1
+#ifndef _mceik_h__
+#define _mceik_h__ 1   /* the reference's guard (include/mceik.h:1-2): this header replaces it */
 #include <stdint.h>
 #include "mceik_struct.h"
 #include "mceik_eikonal.h"
@@ -29,6 +29,9 @@ typedef struct mceik_mcmc_opts {
     uint32_t seed;             /* Philox key                                 */
     int max_samples;           /* device sample ring capacity (states)       */
     int device;                /* HIP device ordinal                         */
+    int precision;             /* FSM arithmetic: 32 (0 = default) or 64; tables are fp32 at rest
+                                  either way (fsm3d.f90:1855-1875)           */
+    int max_waves;             /* cap on resident FSM waves (0 = occupancy x CUs) */
 } mceik_mcmc_opts;
 
 /* v0: host [nchains][ncell] int m/s, ncell = ceil(nx/nrefx)*ceil(ny/nrefy)*
@@ -38,18 +41,32 @@ int mceik_mcmc_init(const struct mceik_parms_struct *parms,
                     const struct mceik_catalog_struct *catalog,
                     const mceik_mcmc_opts *opts, const int *v0, mceik_mcmc **out);
 /* Enqueue nsteps proposals for every chain (propose -> FSM -> misfit ->
- * Metropolis); keeps states per mcparms (nburnIn, keepK). Asynchronous. */
+ * Metropolis); keeps states per mcparms (nburnIn, keepK). Asynchronous.
+ * nsteps < 0: run the remaining mcparms.niter - step proposals (mceik_struct.h:58). */
 int mceik_mcmc_run(mceik_mcmc *s, int nsteps);
 int mceik_mcmc_set_stream(mceik_mcmc *s, void *stream);
 int mceik_mcmc_sync(mceik_mcmc *s);
 /* Host copies of the chain state. Any pointer may be NULL. */
 int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long long *naccept, long long *step);
-/* Kept samples: copies up to max states (device or host pointers via kind:
- * 0 host, 1 device); returns the count in *nkept. Layout [k][nchains][ncell]. */
+/* Kept samples: copies the n = min(max, kept, max_samples) most recent kept
+ * states, oldest first, into v_out [n][nchains][ncell] and logl_out
+ * [n][nchains] (both host memory for kind 0, both device memory for kind 1);
+ * returns n in *nkept. */
 int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max, int kind, int *nkept);
-/* Diagnostics of the last step: device pointers (travel-time table, per-solve
- * iteration counts, accept flags) and sizes. */
-int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept);
+/* Diagnostics of the last step: device pointers to the travel-time table
+ * [nchains][nstat][nev] (fp32), per-solve iteration counts and reference ierr
+ * [nchains][nstat] (int), and accept flags [nchains].  Any pointer may be NULL. */
+int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept,
+                    const int **ierr);
+/* Checkpoint / resume.  The proposal RNG is Philox keyed by (global chain,
+ * step), so (v, logl, naccept, step, nkept) is the complete chain state:
+ * restoring it into a sampler built with the same problem, seed and chain
+ * shard continues the chains bit for bit.  checkpoint: host copies
+ * (synchronises; any pointer may be NULL).  restore: host arrays for this
+ * sampler's chains; logl == NULL recomputes it with one forward. */
+int mceik_mcmc_checkpoint(mceik_mcmc *s, int *v, double *logl, long long *naccept, long long *step, int *nkept);
+int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *logl, const long long *naccept,
+                       long long step, int nkept);
 /* FSM accounting since init (or the last reset): kernel time of every FSM
  * launch from hipEvents on the sampler's stream (ms), launches, and the
  * sum over solves of executed iterations (8 sweeps each) and visits[3] = brick

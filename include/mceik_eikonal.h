@@ -99,6 +99,9 @@ typedef struct mceik_fsm_batch {
                                    only the order solves start in changes), or NULL = model-major */
     unsigned long long *solve_clock; /* device [nmodel*nstat][2]: s_memrealtime (100 MHz) at the
                                         start and end of each solve (diagnostic), or NULL */
+    int max_waves;              /* cap on the resident solve waves (0 = occupancy x CUs); with fewer
+                                   waves than solves each wave runs several solves in its reused
+                                   scratch field (the production path at C2/C3) */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */

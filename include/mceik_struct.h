@@ -7,8 +7,8 @@
  * tests/test_capi.py checks sizeof/offsetof of every struct against the
  * layout the reference header implies.
  */
-#ifndef MCEIK_STRUCT_H_AMD
-#define MCEIK_STRUCT_H_AMD 1
+#ifndef _mceik_struct_h__
+#define _mceik_struct_h__ 1   /* the reference's own guard: one definition when both are included */
 
 /* phase of an observation (mceik_struct.h:4-8) */
 enum pick_type_enum {

@@ -23,7 +23,8 @@ class FsmBatch(C.Structure):
                 ("nev", C.c_int), ("ev_node", C.c_void_p), ("ttab", C.c_void_p),
                 ("u_out", C.c_void_p), ("niter", C.c_void_p), ("ierr", C.c_void_p),
                 ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
-                ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p)]
+                ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p),
+                ("max_waves", C.c_int)]
 
 
 class RelocateBatch(C.Structure):
@@ -71,7 +72,8 @@ class McmcOpts(C.Structure):
     """mceik_mcmc_opts (include/mceik.h)."""
     _fields_ = [("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nchains", C.c_int),
                 ("chain_offset", C.c_int), ("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int),
-                ("seed", C.c_uint32), ("max_samples", C.c_int), ("device", C.c_int)]
+                ("seed", C.c_uint32), ("max_samples", C.c_int), ("device", C.c_int),
+                ("precision", C.c_int), ("max_waves", C.c_int)]
 
 
 # every extern "C" symbol include/*.h declares
@@ -80,7 +82,7 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "locate_l2_g
            "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
-           "mceik_mcmc_finalize")
+           "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize")
 
 
 def lib():
@@ -125,7 +127,11 @@ def lib():
     L.mceik_mcmc_get_samples.restype = C.c_int
     L.mceik_mcmc_get_samples.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, pi]
     L.mceik_mcmc_last.restype = C.c_int
-    L.mceik_mcmc_last.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 3
+    L.mceik_mcmc_last.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 4
+    L.mceik_mcmc_checkpoint.restype = C.c_int
+    L.mceik_mcmc_checkpoint.argtypes = [C.c_void_p] + [C.c_void_p] * 3 + [C.POINTER(C.c_longlong), pi]
+    L.mceik_mcmc_restore.restype = C.c_int
+    L.mceik_mcmc_restore.argtypes = [C.c_void_p] + [C.c_void_p] * 3 + [C.c_longlong, C.c_int]
     L.mceik_mcmc_fsm_stats.restype = C.c_int
     L.mceik_mcmc_fsm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong),
                                        C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]

@@ -105,6 +105,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.visit_stats = b->visit_stats;
     L.solve_order = b->solve_order;
     L.solve_clock = b->solve_clock;
+    L.max_waves = b->max_waves;
 }
 
 static int g_device_cus = 0;
@@ -150,6 +151,7 @@ static int batch_waves(const FsmLaunch &L, int is_double)
     static const int env_cap = [] { const char *e = getenv("MCEIK_WAVES_PER_CU"); return e ? atoi(e) : 0; }();
     if (env_cap > 0 && env_cap < per_cu) per_cu = env_cap;
     long w = (long)per_cu * device_cus();
+    if (L.max_waves > 0 && w > L.max_waves) w = L.max_waves;
     if (w > L.nsolve) w = L.nsolve;
     return (int)(w < 1 ? 1 : w);
 }
@@ -205,7 +207,7 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
                                      void *stream)
 {
     if (!b || b->nx < 2 || b->ny < 2 || b->nz < 2 || b->nx > 4096 || b->ny > 4096 || b->nz > 4096 ||
-        b->nsrc < 1 || b->nsrc > MCEIK_MAX_SRC ||
+        b->nsrc < 1 ||
         b->nmodel < 1 || b->nstat < 1 || !(b->precision == 32 || b->precision == 64)) {
         fprintf(stderr, "mceik_fsm_batch_solve: invalid batch description\n");
         return 1;
@@ -290,8 +292,8 @@ static void serial_driver(int is_double, const int *job, const int *iverb, const
         return;
     }
     if (!linit) { printf(" eikonal3d_serial_driver: Solver not initalized!\n"); *ierr = 1; return; }
-    if (*nsrc < 1 || *nsrc > MCEIK_MAX_SRC) {
-        printf(" eikonal3d_serial_driver: nsrc must be in [1,%d]\n", MCEIK_MAX_SRC);
+    if (*nsrc < 1) {
+        printf(" eikonal3d_serial_driver: nsrc must be >= 1\n");
         *ierr = 1;
         return;
     }
@@ -510,19 +512,39 @@ extern "C" int mceik_relocate(const mceik_relocate_batch *b, void *stream)
 
 // ---------------------------------------------------------------------------
 // MCMC sampler (include/mceik.h)
+#define MCEIK_EV_RING 32           // hipEvent pairs around timed FSM launches (fixed ring)
+
 struct mceik_mcmc {
     McmcDev D;
-    std::vector<hipEvent_t> ev;        // pairs around FSM launches (timing)
-    size_t ev_used;
-    long long nlaunch;
+    hipEvent_t ev[2 * MCEIK_EV_RING];  // pairs around FSM launches (timing)
+    int ev_made;                       // pairs created so far
+    long long nlaunch;                 // timed launches since the last reset
+    long long ev_folded;               // launches whose pair has been folded into fsm_ms
+    double fsm_ms;                     // folded kernel time (ms)
     unsigned long long *d_iters;
+    int *d_ierr;
     mceik_fsm_batch fb;
-    int device, max_samples, nburn, keepk, nkept;
+    int device, max_samples, nburn, keepk, nkept, niter_total;
+    int nkept_base;                    // nkept at the last restore: earlier states are not in the ring
     long long step;
     hipStream_t stream;
     void *ws;
     size_t ws_bytes;
     std::vector<void *> allocs;
+};
+
+// Every entry point runs on the sampler's device and restores the caller's.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceScope()
+    {
+        if (prev >= 0) hipSetDevice(prev);
+    }
 };
 
 template <typename T>
@@ -551,25 +573,63 @@ static int source_index(int n, double x0, double dx, double xs)   // fsm3d.f90:6
     return (int)((xs - x0) / dx + 0.5);
 }
 
+// Adds the elapsed time of timed launch k (its pair is complete once its end
+// event is) to fsm_ms.  Blocks only when MCEIK_EV_RING launches are queued.
+static int fold_launch(mceik_mcmc *s, long long k)
+{
+    const int r = (int)(k % MCEIK_EV_RING);
+    float t = 0.f;
+    HIPCHK(hipEventSynchronize(s->ev[2 * r + 1]));
+    HIPCHK(hipEventElapsedTime(&t, s->ev[2 * r], s->ev[2 * r + 1]));
+    s->fsm_ms += t;
+    return 0;
+}
+
 static int mcmc_forward(mceik_mcmc *s, bool timed)
 {
+    int r = 0;
     if (timed) {
-        if (s->ev_used + 2 > s->ev.size()) {
-            for (int i = 0; i < 64; i++) {
-                hipEvent_t e;
-                HIPCHK(hipEventCreate(&e));
-                s->ev.push_back(e);
-            }
+        // the ring slot of launch nlaunch - RING is reused: fold that launch first
+        while (s->ev_folded <= s->nlaunch - MCEIK_EV_RING) {
+            if (fold_launch(s, s->ev_folded)) return -1;
+            s->ev_folded++;
         }
-        HIPCHK(hipEventRecord(s->ev[s->ev_used], s->stream));
+        r = (int)(s->nlaunch % MCEIK_EV_RING);
+        while (s->ev_made <= r) {
+            HIPCHK(hipEventCreate(&s->ev[2 * s->ev_made]));
+            HIPCHK(hipEventCreate(&s->ev[2 * s->ev_made + 1]));
+            s->ev_made++;
+        }
+        HIPCHK(hipEventRecord(s->ev[2 * r], s->stream));
     }
     if (mceik_fsm_batch_solve(&s->fb, s->ws, s->ws_bytes, s->stream)) return -1;
     if (timed) {
-        HIPCHK(hipEventRecord(s->ev[s->ev_used + 1], s->stream));
-        s->ev_used += 2;
+        HIPCHK(hipEventRecord(s->ev[2 * r + 1], s->stream));
         s->nlaunch++;
     }
     return 0;
+}
+
+// After a forward: every solve's reference ierr must be 0 (a station on the
+// grid's first node is the SETBCS quirk, fsm3d.f90:736-745, ierr = 1; its table
+// would stay u_nan).  Synchronises; names the failing stations.
+static int check_forward_ierr(mceik_mcmc *s, const char *who)
+{
+    const size_t n = (size_t)s->D.nchains * s->D.nstat;
+    std::vector<int> ie(n);
+    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipMemcpy(ie.data(), s->d_ierr, n * sizeof(int), hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int st = 0; st < s->D.nstat; st++) {
+        int e = 0;
+        for (int c = 0; c < s->D.nchains && !e; c++) e = ie[(size_t)c * s->D.nstat + st];
+        if (e) {
+            fprintf(stderr, "%s: station %d (0-based): eikonal solve ierr = %d%s\n", who, st, e,
+                    e == 1 ? " (source on the grid's first node or outside it, fsm3d.f90:736-745)" : "");
+            bad = 1;
+        }
+    }
+    return bad;
 }
 
 extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const struct mceik_stations_struct *st,
@@ -583,10 +643,22 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         return 1;
     }
     if (o->nx < 2 || o->ny < 2 || o->nz < 2 || o->nchains < 1 || st->nstat < 1 || cat->nevents < 1 ||
-        o->vmin < 1 || o->vmax < o->vmin || o->dvmax < 1) {
+        o->vmin < 1 || o->vmax < o->vmin || o->dvmax < 1 || !(o->precision == 0 || o->precision == 32 ||
+                                                              o->precision == 64)) {
         fprintf(stderr, "mceik_mcmc_init: invalid options\n");
         return 1;
     }
+    for (int e = 0; e < cat->nevents; e++)
+        if (cat->obsPtr[e + 1] < cat->obsPtr[e]) {
+            fprintf(stderr, "mceik_mcmc_init: obsPtr must be non-decreasing\n");
+            return 1;
+        }
+    for (int j = 0; j < cat->obsPtr[cat->nevents]; j++)
+        if (cat->luseObs[j] != 0 && cat->pickType[j] == P_PRIMARY_PICK && !(cat->varObs[j] > 0.0)) {
+            fprintf(stderr, "mceik_mcmc_init: observation %d has varObs <= 0\n", j);
+            return 1;
+        }
+    DeviceScope dg(o->device);
     if (hipSetDevice(o->device) != hipSuccess) return -1;
     mceik_mcmc *s = new mceik_mcmc();
     s->device = o->device;
@@ -595,6 +667,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     s->nkept = 0;
     s->nburn = parms->mcparms.nburnIn;
     s->keepk = parms->mcparms.keepK > 0 ? parms->mcparms.keepK : 1;
+    s->niter_total = parms->mcparms.niter;
     s->max_samples = o->max_samples > 0 ? o->max_samples : 0;
     int nrx = parms->nrefx > 0 ? parms->nrefx : 1, nry = parms->nrefy > 0 ? parms->nrefy : 1,
         nrz = parms->nrefz > 0 ? parms->nrefz : 1;
@@ -633,7 +706,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     double *d_src = nullptr;
     int *d_ev = nullptr, *d_optr = nullptr;
     float *d_tt = nullptr;
-    int *d_niter = nullptr, *d_ierr = nullptr;
+    int *d_niter = nullptr;
     rc |= dput(s, &d_src, src.data(), src.size());
     rc |= dput(s, &d_ev, ev.data(), ev.size());
     rc |= dput(s, &d_optr, (const int *)cat->obsPtr, (size_t)nev + 1);
@@ -656,7 +729,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     rc |= dalloc(s, &D.accept, nch);
     rc |= dalloc(s, &d_tt, (size_t)nch * nstat * nev);
     rc |= dalloc(s, &d_niter, (size_t)nch * nstat);
-    rc |= dalloc(s, &d_ierr, (size_t)nch * nstat);
+    rc |= dalloc(s, &s->d_ierr, (size_t)nch * nstat);
     rc |= dalloc(s, &s->d_iters, 4);          // [0] iterations, [1..3] visit_stats
     if (s->max_samples) {
         rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncell);
@@ -669,14 +742,17 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     memset(&b, 0, sizeof(b));
     b.nx = o->nx; b.ny = o->ny; b.nz = o->nz; b.h = parms->dx;
     b.x0 = parms->x0; b.y0 = parms->y0; b.z0 = parms->z0;
-    b.maxit = parms->eikparms.maxit; b.tol = parms->eikparms.tol; b.precision = 32;
+    b.maxit = parms->eikparms.maxit; b.tol = parms->eikparms.tol;
+    b.precision = o->precision == 64 ? 64 : 32;
     b.nmodel = nch; b.nstat = nstat; b.nsrc = 1; b.src = d_src;
     b.slow_mode = 1; b.slow = D.slow_prop; b.nrx = nrx; b.nry = nry; b.nrz = nrz;
-    b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = d_ierr;
+    b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = s->d_ierr;
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
     b.visit_stats = s->d_iters + 1;
-    b.fast_sqrt = parms->dx / (double)o->vmax >= 1e-12 ? 1 : 0;   // f = h/v stays a normal float
+    b.max_waves = o->max_waves > 0 ? o->max_waves : 0;
+    // f = h/v stays a normal float: the short correctly rounded sqrt (fp32 only)
+    b.fast_sqrt = b.precision == 32 && parms->dx / (double)o->vmax >= 1e-12 ? 1 : 0;
     s->ws_bytes = mceik_fsm_workspace_bytes(&b);
     if (hipMalloc(&s->ws, s->ws_bytes) != hipSuccess) {
         fprintf(stderr, "mceik_mcmc_init: cannot allocate %zu B of FSM workspace\n", s->ws_bytes);
@@ -699,6 +775,10 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         return -1;
     }
     b.solve_clock = nullptr;
+    if (check_forward_ierr(s, "mceik_mcmc_init")) {
+        mceik_mcmc_finalize(&s);
+        return 2;
+    }
     if (report) {
         std::vector<unsigned long long> clk((size_t)nch * nstat * 2);
         if (hipMemcpy(clk.data(), d_clock, clk.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -732,7 +812,12 @@ extern "C" int mceik_mcmc_set_stream(mceik_mcmc *s, void *stream)
 
 extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
 {
-    if (!s || nsteps < 0) return 1;
+    if (!s) return 1;
+    if (nsteps < 0) {
+        const long long left = (long long)s->niter_total - s->step;
+        nsteps = left > 0 ? (int)left : 0;
+    }
+    DeviceScope dg(s->device);
     for (int i = 0; i < nsteps; i++) {
         uint64_t step = (uint64_t)s->step;
         HIPCHK(mcmc_propose(s->D, step, s->stream));
@@ -751,6 +836,7 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
 extern "C" int mceik_mcmc_sync(mceik_mcmc *s)
 {
     if (!s) return 1;
+    DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
     return 0;
 }
@@ -758,6 +844,7 @@ extern "C" int mceik_mcmc_sync(mceik_mcmc *s)
 extern "C" int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long long *naccept, long long *step)
 {
     if (!s) return 1;
+    DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
     const McmcDev &D = s->D;
     if (v) HIPCHK(hipMemcpy(v, D.v, (size_t)D.nchains * D.ncell * 4, hipMemcpyDeviceToHost));
@@ -767,27 +854,88 @@ extern "C" int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long lo
     return 0;
 }
 
-extern "C" int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max, int kind, int *nkept)
+extern "C" int mceik_mcmc_checkpoint(mceik_mcmc *s, int *v, double *logl, long long *naccept, long long *step,
+                                     int *nkept)
 {
     if (!s) return 1;
-    int have = s->nkept < s->max_samples ? s->nkept : s->max_samples;
-    int n = have < max ? have : max;
-    if (nkept) *nkept = n;
-    if (n <= 0) return 0;
-    HIPCHK(hipStreamSynchronize(s->stream));
-    hipMemcpyKind k = kind ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    size_t per = (size_t)s->D.nchains * s->D.ncell;
-    if (v_out) HIPCHK(hipMemcpy(v_out, s->D.keep_v, (size_t)n * per * 4, k));
-    if (logl_out) HIPCHK(hipMemcpy(logl_out, s->D.keep_logl, (size_t)n * s->D.nchains * 8, hipMemcpyDeviceToHost));
+    if (mceik_mcmc_get_state(s, v, logl, naccept, step)) return -1;
+    if (nkept) *nkept = s->nkept;
     return 0;
 }
 
-extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept)
+extern "C" int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *logl, const long long *naccept,
+                                  long long step, int nkept)
+{
+    if (!s || !v || step < 0 || nkept < 0) return 1;
+    DeviceScope dg(s->device);
+    McmcDev &D = s->D;
+    const size_t n = (size_t)D.nchains * D.ncell;
+    for (size_t i = 0; i < n; i++)
+        if (v[i] < D.vmin || v[i] > D.vmax) {
+            fprintf(stderr, "mceik_mcmc_restore: v[%zu] = %d outside the prior [%d, %d]\n", i, v[i], D.vmin, D.vmax);
+            return 1;
+        }
+    std::vector<float> sl(n);
+    for (size_t i = 0; i < n; i++) sl[i] = 1.0f / (float)v[i];
+    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipMemcpy(D.v, v, n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D.slow_cur, sl.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D.slow_prop, sl.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    if (naccept) HIPCHK(hipMemcpy(D.naccept, naccept, (size_t)D.nchains * 8, hipMemcpyHostToDevice));
+    else HIPCHK(hipMemset(D.naccept, 0, (size_t)D.nchains * 8));
+    if (logl) {
+        HIPCHK(hipMemcpy(D.logl, logl, (size_t)D.nchains * 8, hipMemcpyHostToDevice));
+    } else {
+        // one forward of the restored models (not timed, not counted in the FSM stats)
+        unsigned long long keep[4];
+        HIPCHK(hipMemcpy(keep, s->d_iters, sizeof(keep), hipMemcpyDeviceToHost));
+        if (mcmc_forward(s, false)) return -1;
+        HIPCHK(mcmc_init_loglik(D, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        HIPCHK(hipMemcpy(s->d_iters, keep, sizeof(keep), hipMemcpyHostToDevice));
+        if (check_forward_ierr(s, "mceik_mcmc_restore")) return 2;
+    }
+    s->step = step;
+    s->nkept = nkept;
+    s->nkept_base = nkept;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max, int kind, int *nkept)
+{
+    if (!s) return 1;
+    int have = std::min(s->nkept - s->nkept_base, s->max_samples);
+    int n = have < max ? have : max;
+    if (nkept) *nkept = n;
+    if (n <= 0) return 0;
+    DeviceScope dg(s->device);
+    HIPCHK(hipStreamSynchronize(s->stream));
+    hipMemcpyKind k = kind ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const size_t per = (size_t)s->D.nchains * s->D.ncell;
+    // ring slot of the i-th of the n most recent states: (nkept - n + i) mod max_samples
+    int i = 0;
+    while (i < n) {
+        const int slot = (int)(((long long)s->nkept - n + i) % s->max_samples);
+        const int run = std::min(n - i, s->max_samples - slot);     // contiguous slots
+        if (v_out)
+            HIPCHK(hipMemcpy((int *)v_out + (size_t)i * per, s->D.keep_v + (size_t)slot * per,
+                             (size_t)run * per * 4, k));
+        if (logl_out)
+            HIPCHK(hipMemcpy(logl_out + (size_t)i * s->D.nchains, s->D.keep_logl + (size_t)slot * s->D.nchains,
+                             (size_t)run * s->D.nchains * 8, k));
+        i += run;
+    }
+    return 0;
+}
+
+extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept,
+                               const int **ierr)
 {
     if (!s) return 1;
     if (ttab) *ttab = s->fb.ttab;
     if (niter) *niter = s->fb.niter;
     if (accept) *accept = s->D.accept;
+    if (ierr) *ierr = s->d_ierr;
     return 0;
 }
 
@@ -795,22 +943,22 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
                                     unsigned long long *visits, int reset)
 {
     if (!s) return 1;
+    DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
-    double ms = 0.0;
-    for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
-        float t = 0.f;
-        HIPCHK(hipEventElapsedTime(&t, s->ev[i], s->ev[i + 1]));
-        ms += t;
+    while (s->ev_folded < s->nlaunch) {
+        if (fold_launch(s, s->ev_folded)) return -1;
+        s->ev_folded++;
     }
     unsigned long long it[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpy(it, s->d_iters, sizeof(it), hipMemcpyDeviceToHost));
-    if (fsm_ms) *fsm_ms = ms;
+    if (fsm_ms) *fsm_ms = s->fsm_ms;
     if (nlaunch) *nlaunch = s->nlaunch;
     if (iters) *iters = it[0];
     if (visits) { visits[0] = it[1]; visits[1] = it[2]; visits[2] = it[3]; }
     if (reset) {
-        s->ev_used = 0;
+        s->fsm_ms = 0.0;
         s->nlaunch = 0;
+        s->ev_folded = 0;
         HIPCHK(hipMemset(s->d_iters, 0, 4 * sizeof(unsigned long long)));
     }
     return 0;
@@ -820,9 +968,10 @@ extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
 {
     if (!ps || !*ps) return 0;
     mceik_mcmc *s = *ps;
+    DeviceScope dg(s->device);
     hipStreamSynchronize(s->stream);
     for (void *p : s->allocs) hipFree(p);
-    for (hipEvent_t e : s->ev) hipEventDestroy(e);
+    for (int i = 0; i < 2 * s->ev_made; i++) hipEventDestroy(s->ev[i]);
     if (s->ws) hipFree(s->ws);
     delete s;
     *ps = nullptr;

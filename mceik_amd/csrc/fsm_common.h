@@ -6,7 +6,6 @@
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
-#define MCEIK_MAX_SRC 8          // point sources per solve (box BCs, fsm3d.f90:762-840)
 #define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
 #define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
 #define MCEIK_KB 4               // bricks per z-block (stream position) when the block tables fit in LDS
@@ -50,12 +49,13 @@ struct FsmLaunch {
     unsigned long long *visit_stats;  // [3] += tile visits, column-segment updates, changed segments; may be null
     const int *solve_order;      // queue slot -> solve id, or null (slot = solve)
     unsigned long long *solve_clock;  // [nsolve][2] realtime at solve start / end, or null
+    int max_waves;               // host only: cap on resident waves (0 = occupancy x CUs)
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 
 // LDS of one solve wave (byte offsets, shared by host and device):
-//  0 BC boxes [MAX_SRC][6] int | 1 cell cache [nr][ccb] float (cached mode) |
+//  0 BC boxes [nsrc][6] int (EIKONAL3D_SETBCS, fsm3d.f90:762-840; no source limit beyond LDS) | 1 cell cache [nr][ccb] float (cached mode) |
 //  2 diagonal tile order int [ntiles] | 3 lastproc int [nblocks] | 4 lastchg int [nblocks] |
 //  5 u0 epoch u16 [nblocks] | 6 stream entries int [nr] + block ids int [nr] | 7 run scratch int [8] |
 //  8 staged f [8][64] R (uncached) | 9+10 halos [32 columns][8] R (two halves of 128 R) |
@@ -68,7 +68,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     const bool cached = L.slow_mode != 0 && L.cell_cache;
     const size_t nt = (size_t)L.ntiles, nb = (size_t)L.nblocks, nr = (size_t)L.nr;
     size_t o = 0;
-    off[0] = o; o += mceik_align16(MCEIK_MAX_SRC * 6 * 4);
+    off[0] = o; o += mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
     off[1] = o; o += cached ? mceik_align16(nr * L.ccb * 4) : 0;
     off[2] = o; o += mceik_align16(nt * 4);
     off[3] = o; o += mceik_align16(nb * 4);

@@ -270,7 +270,7 @@ __device__ __forceinline__ size_t brick_index(const FsmLaunch &L, int x, int y, 
 // Wave-uniform, kept in LDS: box k = {xlo, xhi, ylo, yhi, zlo, zhi} (0-based, inclusive).
 struct BcBoxes {
     int n;
-    int *box;          // LDS, [MCEIK_MAX_SRC][6]
+    int *box;          // LDS, [nsrc][6]
 };
 
 // ---- LDS working set of one solve wave -------------------------------------
@@ -284,7 +284,7 @@ struct BcBoxes {
 // clocks live in LDS.
 template <typename R>
 struct Smem {
-    int *box;                    // BC boxes [MCEIK_MAX_SRC][6]
+    int *box;                    // BC boxes [nsrc][6]
     float *cc;                   // cell cache [nr][ccb]                   (SLOWMODE 2)
     int *order;                  // diagonal tile order: txs | tys << 16   [ntiles]
     int *lastproc, *lastchg;     // per z-block stream clock of the last visit / last visit with a change

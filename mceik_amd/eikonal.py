@@ -153,7 +153,7 @@ class BatchSolver:
         self.nref = nref
         self._ws = None
 
-    def describe(self, nmodel, nstat, nsrc, slow_mode, nev=0, max_sweeps=-1):
+    def describe(self, nmodel, nstat, nsrc, slow_mode, nev=0, max_sweeps=-1, max_waves=0):
         b = _lib.FsmBatch()
         b.nx, b.ny, b.nz = self.nx, self.ny, self.nz
         b.h, b.x0, b.y0, b.z0 = self.h, self.x0, self.y0, self.z0
@@ -165,14 +165,17 @@ class BatchSolver:
         b.nev = nev
         b.max_sweeps = max_sweeps
         b.fast_sqrt = 1 if (self.fast_sqrt and slow_mode == 1) else 0
+        b.max_waves = int(max_waves)
         return b
 
     def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None,
-              solve_order=None, solve_clock=False):
+              solve_order=None, solve_clock=False, max_waves=0):
         """solve_order: optional permutation of the nmodel*nstat solve ids (the
         order the work queues hand them out; results do not depend on it).
         solve_clock: also return out["clock"] [nsolve][2], the device realtime
-        (100 MHz) at the start and end of every solve."""
+        (100 MHz) at the start and end of every solve.  max_waves: cap on the
+        resident solve waves (0 = occupancy x CUs); fewer waves than solves runs
+        the production path (several solves per wave in reused scratch)."""
         import torch
         dev = slow.device
         sources = sources.to(device=dev, dtype=torch.float64).contiguous()
@@ -186,7 +189,7 @@ class BatchSolver:
             raise TypeError("cell slowness must be float32")
         slow = slow.contiguous()
         nev = 0 if ev_node is None else int(ev_node.numel())
-        b = self.describe(nmodel, nstat, nsrc, slow_mode, nev, max_sweeps)
+        b = self.describe(nmodel, nstat, nsrc, slow_mode, nev, max_sweeps, max_waves)
         nsolve = nmodel * nstat
         niter = torch.zeros(nsolve, dtype=torch.int32, device=dev)
         ierr = torch.zeros(nsolve, dtype=torch.int32, device=dev)

@@ -151,7 +151,13 @@ def _fsm_tables(grid, stations, tables, device):
                           device=torch.device("cuda", device))
         bs = BatchSolver(g["nx"], g["ny"], g["nz"], g["dx"], g["x0"], g["y0"], g["z0"], maxit=50, tol=1e-8,
                          precision=64)
-        u = bs.solve(src, slow, want_fields=True)["u"].reshape(len(mine), n).cpu().numpy()
+        res = bs.solve(src, slow, want_fields=True)
+        u = res["u"].reshape(len(mine), n).cpu().numpy()
+        ierr = res["ierr"].cpu().numpy()
+        if np.any(ierr != 0):
+            bad = [(mine[i][0], int(ierr[i])) for i in np.flatnonzero(ierr)]
+            raise RuntimeError(f"eikonal solve failed for (station, ierr) {bad}: a station on the grid's "
+                               "first node is the reference's SETBCS quirk (fsm3d.f90:736-745)")
         for i, key in enumerate(mine):
             out[key] = u[i]
     return out

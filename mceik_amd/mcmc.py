@@ -57,6 +57,7 @@ class Problem:
     seed: int = 2016
     nburn: int = 0
     keepk: int = 1
+    niter: int = 0                  # mcparms.niter: total proposals (Sampler.run(-1) runs the rest)
     v_true: np.ndarray = None       # [ncell] int, model used to make the picks
     _keep: list = field(default_factory=list, repr=False)
 
@@ -131,7 +132,7 @@ class Problem:
 
         parms = _lib.MceikParms()
         parms.mcparms.nburnIn = int(self.nburn)
-        parms.mcparms.niter = 0
+        parms.mcparms.niter = int(self.niter)
         parms.mcparms.keepK = int(self.keepk)
         parms.eikparms.tol = float(self.tol)
         parms.eikparms.maxit = int(self.maxit)
@@ -232,7 +233,8 @@ def shard(nchains_total, rank, world):
 class Sampler:
     """One GPU's chains (include/mceik.h handle)."""
 
-    def __init__(self, p: Problem, nchains, chain_offset=0, v0=None, max_samples=0, device=0):
+    def __init__(self, p: Problem, nchains, chain_offset=0, v0=None, max_samples=0, device=0, precision=32,
+                 max_waves=0):
         self.p = p
         self.nchains = int(nchains)
         self.chain_offset = int(chain_offset)
@@ -247,6 +249,7 @@ class Sampler:
         o.nchains, o.chain_offset = self.nchains, self.chain_offset
         o.vmin, o.vmax, o.dvmax, o.seed = p.vmin, p.vmax, p.dvmax, p.seed
         o.max_samples, o.device = int(max_samples), int(device)
+        o.precision, o.max_waves = int(precision), int(max_waves)
         h = C.c_void_p()
         rc = L.mceik_mcmc_init(C.byref(parms), C.byref(st), C.byref(cat), C.byref(o),
                                self.v0.ctypes.data_as(C.c_void_p), C.byref(h))
@@ -278,19 +281,49 @@ class Sampler:
             raise RuntimeError("mceik_mcmc_get_state failed")
         return v, logl, nacc, step.value
 
-    def last(self):
-        """Host copies of the last step's travel-time table, iteration counts, accept flags."""
-        tt, it, acc = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        self._L.mceik_mcmc_last(self._h, C.byref(tt), C.byref(it), C.byref(acc))
+    def last(self, with_ierr=False):
+        """Host copies of the last step's travel-time table, iteration counts and
+        accept flags (and the per-solve reference ierr if with_ierr)."""
+        tt, it, acc, ie = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._L.mceik_mcmc_last(self._h, C.byref(tt), C.byref(it), C.byref(acc), C.byref(ie))
         p = self.p
         ttab = np.empty((self.nchains, p.nstat, p.nevents), np.float32)
         niter = np.empty((self.nchains, p.nstat), np.int32)
+        ierr = np.empty((self.nchains, p.nstat), np.int32)
         a = np.empty(self.nchains, np.uint8)
         self.sync()
-        for dst, src in ((ttab, tt), (niter, it), (a, acc)):
+        for dst, src in ((ttab, tt), (niter, it), (a, acc), (ierr, ie)):
             if self._L.mceik_memcpy(dst.ctypes.data_as(C.c_void_p), src, dst.nbytes, 1) != 0:
                 raise RuntimeError("mceik_memcpy failed")
-        return ttab, niter, a
+        return (ttab, niter, a, ierr) if with_ierr else (ttab, niter, a)
+
+    def checkpoint(self):
+        """Complete chain state (mceik_mcmc_checkpoint): dict of v, logl, naccept,
+        step, nkept -- restore() into a sampler of the same problem/shard resumes
+        the chains bit for bit."""
+        v = np.empty((self.nchains, self.p.ncell), np.int32)
+        logl = np.empty(self.nchains, np.float64)
+        nacc = np.empty(self.nchains, np.int64)
+        step, nkept = C.c_longlong(0), C.c_int(0)
+        if self._L.mceik_mcmc_checkpoint(self._h, v.ctypes.data_as(C.c_void_p), logl.ctypes.data_as(C.c_void_p),
+                                         nacc.ctypes.data_as(C.c_void_p), C.byref(step), C.byref(nkept)) != 0:
+            raise RuntimeError("mceik_mcmc_checkpoint failed")
+        return {"v": v, "logl": logl, "naccept": nacc, "step": step.value, "nkept": nkept.value,
+                "chain_offset": self.chain_offset, "seed": self.p.seed}
+
+    def restore(self, ck, recompute_logl=False):
+        """Load a checkpoint() dict (mceik_mcmc_restore)."""
+        if ck.get("chain_offset", self.chain_offset) != self.chain_offset or ck.get("seed", self.p.seed) != self.p.seed:
+            raise ValueError("checkpoint belongs to another chain shard or seed")
+        v = np.ascontiguousarray(ck["v"], dtype=np.int32)
+        assert v.shape == (self.nchains, self.p.ncell)
+        logl = None if recompute_logl else np.ascontiguousarray(ck["logl"], dtype=np.float64)
+        nacc = np.ascontiguousarray(ck["naccept"], dtype=np.int64)
+        rc = self._L.mceik_mcmc_restore(self._h, v.ctypes.data_as(C.c_void_p),
+                                        None if logl is None else logl.ctypes.data_as(C.c_void_p),
+                                        nacc.ctypes.data_as(C.c_void_p), int(ck["step"]), int(ck.get("nkept", 0)))
+        if rc != 0:
+            raise RuntimeError(f"mceik_mcmc_restore failed ({rc})")
 
     def fsm_stats(self, reset=False):
         """(FSM kernel ms from hipEvents, launches, executed iterations summed over
@@ -340,3 +373,45 @@ def picks_from_forward(device=0, precision=64):
         torch.cuda.synchronize(dev)
         return out["ttab"].cpu().numpy().reshape(p.nstat, p.nevents)
     return f
+
+
+def gather_kept(smp: Sampler, nchains_total, group=None, dst=0, device=None):
+    """Checkpoint gather (SURVEY s.8e): the most recent kept state of every
+    chain on every rank -> rank `dst`, in global chain order.
+
+    One process per GPU; `smp` holds this rank's shard `shard(nchains_total,
+    rank, world)`.  With `device` (a torch CUDA device) the states move as
+    device tensors -- over RCCL for an nccl group, xGMI on one node -- else as
+    host tensors (gloo).  Shards are padded to the largest one, as gather
+    needs equal sizes.  Returns (v [nchains_total, ncell] int32, logl
+    [nchains_total] float64) torch tensors on `dst`, (None, None) elsewhere."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    width = -(-nchains_total // world)
+    ncell = smp.p.ncell
+    if device is not None:
+        v = torch.zeros((width, ncell), dtype=torch.int32, device=device)
+        lg = torch.zeros((width,), dtype=torch.float64, device=device)
+        got = C.c_int(0)
+        rc = smp._L.mceik_mcmc_get_samples(smp._h, C.c_void_p(v.data_ptr()), C.c_void_p(lg.data_ptr()), 1, 1,
+                                           C.byref(got))
+        if rc != 0 or got.value != 1:
+            raise RuntimeError("mceik_mcmc_get_samples: no kept state to gather")
+    else:
+        kv, kl = smp.samples(max_states=1)
+        if len(kv) == 0:
+            raise RuntimeError("no kept state to gather (max_samples = 0 or still in burn-in)")
+        v = torch.zeros((width, ncell), dtype=torch.int32)
+        lg = torch.zeros((width,), dtype=torch.float64)
+        v[:smp.nchains] = torch.from_numpy(kv[0])
+        lg[:smp.nchains] = torch.from_numpy(kl[0])
+    gv = [torch.empty_like(v) for _ in range(world)] if rank == dst else None
+    gl = [torch.empty_like(lg) for _ in range(world)] if rank == dst else None
+    dist.gather(v, gv, dst=dst, group=group)
+    dist.gather(lg, gl, dst=dst, group=group)
+    if rank != dst:
+        return None, None
+    parts = [shard(nchains_total, r, world) for r in range(world)]
+    return (torch.cat([gv[r][:hi - lo] for r, (lo, hi) in enumerate(parts)]),
+            torch.cat([gl[r][:hi - lo] for r, (lo, hi) in enumerate(parts)]))

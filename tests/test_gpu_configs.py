@@ -1,0 +1,194 @@
+"""Parity at the BASELINE.json configurations (SURVEY s.8 table), on the GPU.
+
+Every test runs the kernel instance the bench or the sampler actually runs at
+that geometry and compares with the oracle (oracle/fsm_impl.inc fp32 twin,
+oracle_mcmc_run) bit for bit:
+
+* C1  1 chain, 32^3 homogeneous, 4 stations, 100 proposals (the plumbing case)
+* C2  256 chains x 16 stations at 64^3: 4096 solves on at most 2048 waves,
+      so waves run several solves in their reused scratch field
+* C3  128^3, 32 stations, 32 events: the bench's instance
+      fsm_solve_kernel<float, 2, true, 2, 1, 4> (cells, LDS cell cache, short
+      sqrt, compile-time kb = 4, 1024 z-blocks = MCEIK_MAX_BLOCKS), with fewer
+      resident waves than solves; then two MCMC steps
+* C5  256^3 (8 x 8 x 8-brick columns: the runtime-kb kernel with 32-brick
+      z-blocks), two full fields
+C4 is C3's geometry sharded over 8 GPUs (the driver's scaling run).
+The CPU side uses the oracle's OpenMP (one solve per thread).
+"""
+import concurrent.futures as cf
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _problem(config, **kw):
+    from mceik_amd import mcmc
+    return mcmc.make_problem(config, picks=mcmc.picks_from_forward(0), **kw)
+
+
+def test_c3_sampler_forward_bitwise_reused_scratch():
+    """C3 geometry through the sampler's own launch (the bench instance): the
+    initial forward's travel-time tables and iteration counts of 4 chains x
+    32 stations equal the fp32 twin bit for bit.  max_waves = 16 puts 8 solves
+    on every wave, one after another in the wave's reused u / u0 scratch."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("C3")
+    assert (p.nx, p.nstat, p.nevents) == (128, 32, 32)
+    s = mcmc.Sampler(p, nchains=4, chain_offset=100, max_waves=16)
+    v0, logl0, _, _ = s.state()
+    ttab, niter, _, ierr = s.last(with_ierr=True)
+    s.close()
+    assert not ierr.any()
+    P = O.make_problem(p)
+    for c in range(4):
+        tt, it = O.forward_f32(P, v0[c])
+        assert np.array_equal(ttab[c].view(np.uint32), tt.view(np.uint32)), c
+        assert np.array_equal(niter[c], it), c
+        assert logl0[c] == O.loglik(P, tt)
+
+
+def test_c3_mcmc_two_steps_bitwise():
+    """Two MCMC steps of 2 chains at C3 geometry: accept sequence, logL trace
+    and chain models bitwise = oracle_mcmc_run."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("C3")
+    p.dvmax = 400
+    p.var[:] = 1e-6
+    off, nch, nsteps = 517, 2, 2
+    s = mcmc.Sampler(p, nchains=nch, chain_offset=off)
+    v0, logl0, _, _ = s.state()
+    acc, trace = [], []
+    for _ in range(nsteps):
+        s.run(1)
+        _, _, a = s.last()
+        _, lg, _, _ = s.state()
+        acc.append(a.copy())
+        trace.append(lg.copy())
+    v, logl, nacc, step = s.state()
+    s.close()
+    vo, lo, acco, traceo = O.mcmc_run(O.make_problem(p), v0, logl0, off, 0, nsteps)
+    assert np.array_equal(np.array(acc), acco)
+    assert np.array_equal(np.array(trace).view(np.uint64), traceo.view(np.uint64))
+    assert np.array_equal(v, vo)
+    assert np.array_equal(logl.view(np.uint64), lo.view(np.uint64))
+    assert step == nsteps and nacc.sum() == acco.sum()
+
+
+def test_c2_workload_sampled_chains():
+    """C2: 256 chains x 16 stations at 64^3 in one sampler (4096 solves per
+    step, more than the resident waves); chains 0-3 and 252-255 after two
+    steps equal oracle_mcmc_run bitwise."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("C2")
+    assert (p.nx, p.nstat, p.nevents) == (64, 16, 16)
+    p.dvmax = 400
+    p.var[:] = 1e-6
+    s = mcmc.Sampler(p, nchains=256)
+    v0, logl0, _, _ = s.state()
+    s.run(2)
+    v, logl, _, _ = s.state()
+    s.close()
+    P = O.make_problem(p)
+    for lo in (0, 252):
+        sl = slice(lo, lo + 4)
+        tt, _ = O.forward_f32(P, v0[lo])
+        assert logl0[lo] == O.loglik(P, tt)
+        vo, lgo, _, _ = O.mcmc_run(P, v0[sl], logl0[sl], lo, 0, 2)
+        assert np.array_equal(v[sl], vo), lo
+        assert np.array_equal(logl[sl].view(np.uint64), lgo.view(np.uint64)), lo
+
+
+def test_c1_plumbing_100_proposals():
+    """C1: 1 chain, 32^3 homogeneous (2000 m/s, h = 1000 m), 4 stations,
+    4 events, 100 proposals through the sampler == oracle_mcmc_run."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("C1")
+    assert (p.nx, p.nstat, p.nevents, p.h) == (32, 4, 4, 1000.0)
+    assert (p.v_true == 2000).all()
+    p.dvmax = 400
+    p.var[:] = 1e-4
+    s = mcmc.Sampler(p, nchains=1)
+    v0, logl0, _, _ = s.state()
+    s.run(100)
+    v, logl, nacc, step = s.state()
+    s.close()
+    vo, lo, acc, _ = O.mcmc_run(O.make_problem(p), v0, logl0, 0, 0, 100)
+    assert step == 100
+    assert np.array_equal(v, vo)
+    assert np.array_equal(logl.view(np.uint64), lo.view(np.uint64))
+    assert nacc[0] == acc.sum() and 0 < acc.sum() < 100
+
+
+def _cells_field(nx, ny, nz, nref, seed):
+    ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
+    v = np.random.default_rng(seed).integers(2500, 6500, (ncz, ncy, ncx)).astype(np.int32)
+    scell = (1.0 / v.astype(np.float32)).astype(np.float32)
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    return scell, scell[k // nref[2], j // nref[1], i // nref[0]].ravel()
+
+
+def test_c5_256cube_fields_bitwise():
+    """C5 geometry: two stations on a 256^3 cell model (runtime-kb kernel,
+    32-brick z-blocks), both full fields and iteration counts == twin."""
+    dev = _dev()
+    n, h, nref = 256, 100.0, (4, 4, 4)
+    scell, sfield = _cells_field(n, n, n, nref, 21)
+    src = np.array([[[0.0, 12345.6, 6543.2, (n - 1) * h]], [[0.0, 3000.0, 22000.0, (n - 1) * h]]])
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(n, n, n, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=True)
+    out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(1, -1), device=dev), want_fields=True)
+    u = out["u"].cpu().numpy().reshape(2, -1)
+    niter = out["niter"].cpu().numpy()
+    del out
+    with cf.ThreadPoolExecutor(2) as ex:       # ctypes releases the GIL: 2 solves in parallel
+        res = list(ex.map(lambda s: O.eikonal_solve(n, n, n, sfield, h, src[s], dtype=np.float32), range(2)))
+    for s, (t, ierr, it) in enumerate(res):
+        assert ierr == 0
+        assert np.array_equal(u[s].view(np.uint32), t.view(np.uint32)), s
+        assert int(niter[s]) == it
+
+
+def test_cells_fast_many_solves_per_wave():
+    """Production path at a moderate size: 16 models x 8 stations (40^3, cells,
+    short sqrt, kb = 4) on 8 waves -- 16 solves per wave in its reused scratch
+    (slot = wave, u0 guarded by the per-block epochs only); every table and
+    iteration count == twin."""
+    dev = _dev()
+    n, h, nref, nmodel, nstat = 40, 100.0, (4, 4, 4), 16, 8
+    rng = np.random.default_rng(4)
+    cells, fields = zip(*[_cells_field(n, n, n, nref, 100 + m) for m in range(nmodel)])
+    src = np.stack([np.array([[0.0, rng.uniform(250, 3650), rng.uniform(250, 3650), (n - 1) * h]])
+                    for _ in range(nstat)])
+    ev = rng.integers(0, n ** 3, 24).astype(np.int32)
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(n, n, n, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=True)
+    out = bs.solve(torch.tensor(src), torch.tensor(np.stack(cells).reshape(nmodel, -1), device=dev),
+                   ev_node=torch.tensor(ev), max_waves=8)
+    tt = out["ttab"].cpu().numpy().reshape(nmodel, nstat, -1)
+    niter = out["niter"].cpu().numpy().reshape(nmodel, nstat)
+
+    def twin(ms):
+        m, s = ms
+        return O.eikonal_solve(n, n, n, fields[m], h, src[s], dtype=np.float32)
+    with cf.ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(twin, [(m, s) for m in range(nmodel) for s in range(nstat)]))
+    for k, (t, _, it) in enumerate(res):
+        m, s = divmod(k, nstat)
+        assert np.array_equal(tt[m, s].view(np.uint32), t[ev].view(np.uint32)), (m, s)
+        assert niter[m, s] == it, (m, s)

@@ -252,11 +252,12 @@ def test_fp32_128cube_vs_twin_and_fp64():
     bs = _solver(n, n, n, h, 32)
     out = bs.solve(torch.tensor(src), torch.tensor(slow32.reshape(1, n, n, n), device=dev), want_fields=True)
     u = out["u"].cpu().numpy().reshape(2, -1)
-    t, _, it = O.eikonal_solve(n, n, n, slow32, h, src[0], dtype=np.float32)
-    assert np.array_equal(u[0].view(np.uint32), t.view(np.uint32))
-    assert int(out["niter"][0]) == it
-    r, _, _ = O.eikonal_solve(n, n, n, slow64, h, src[0])
-    assert np.all(np.abs(u[0] - r) <= 1e-6 * r + 1e-7)
+    for s in range(2):
+        t, _, it = O.eikonal_solve(n, n, n, slow32, h, src[s], dtype=np.float32)
+        assert np.array_equal(u[s].view(np.uint32), t.view(np.uint32)), s
+        assert int(out["niter"][s]) == it
+        r, _, _ = O.eikonal_solve(n, n, n, slow64, h, src[s])
+        assert np.all(np.abs(u[s] - r) <= 1e-6 * r + 1e-7), s
 
 
 def test_locate_l2_gpu_bitwise_vs_reference():

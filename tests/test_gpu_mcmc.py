@@ -145,3 +145,76 @@ def test_posterior_h5io_files(tmp_path):
             lp = f.read_logjpdf(models.shape[0], e + 1)                # the true model
             assert int(np.argmax(lp)) == int(p.ev_node[e])
             assert lp.max() <= 0.0
+
+
+def test_checkpoint_restore_bitwise():
+    """6 steps == 3 steps + checkpoint + restore into a fresh sampler + 3 steps
+    (Philox is keyed by (global chain, step): the checkpoint is the complete
+    state), with the stored logL and with logL recomputed by one forward."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem(seed=9)
+    p.nburn, p.keepk = 0, 1
+    full = mcmc.Sampler(p, nchains=3, chain_offset=7, max_samples=8)
+    full.run(6)
+    vf, lf, af, sf = full.state()
+    kf, klf = full.samples()
+    full.close()
+    a = mcmc.Sampler(p, nchains=3, chain_offset=7, max_samples=8)
+    a.run(3)
+    ck = a.checkpoint()
+    a.close()
+    assert ck["step"] == 3 and ck["nkept"] == 3
+    for recompute in (False, True):
+        b = mcmc.Sampler(p, nchains=3, chain_offset=7, max_samples=8)
+        b.restore(ck, recompute_logl=recompute)
+        b.run(3)
+        vb, lb, ab, sb = b.state()
+        kb, klb = b.samples()
+        b.close()
+        assert sb == sf == 6
+        assert np.array_equal(vb, vf) and np.array_equal(lb.view(np.uint64), lf.view(np.uint64))
+        assert np.array_equal(ab, af)
+        # the restored sampler kept only steps 3..5 (its ring slots 3..5)
+        assert len(kb) == 3 and np.array_equal(kb, kf[3:6]) and np.array_equal(klb, klf[3:6])
+
+
+def test_run_to_niter_and_sample_ring_order():
+    """run(-1) runs the remaining mcparms.niter proposals; once the sample ring
+    wraps, get_samples returns the most recent states oldest first."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem(seed=13)
+    p.nburn, p.keepk, p.niter = 0, 1, 5
+    s = mcmc.Sampler(p, nchains=2, max_samples=2)
+    states = []
+    s.run(2)
+    states += [s.state()[0]]
+    s.run(-1)                                       # steps 2, 3, 4
+    v, _, _, step = s.state()
+    assert step == 5
+    kv, _ = s.samples()
+    s.run(-1)                                       # nothing left
+    assert s.state()[3] == 5
+    s.close()
+    ref = mcmc.Sampler(p, nchains=2)
+    seq = []
+    for _ in range(5):
+        ref.run(1)
+        seq.append(ref.state()[0])
+    ref.close()
+    assert np.array_equal(v, seq[4])
+    assert len(kv) == 2 and np.array_equal(kv[0], seq[3]) and np.array_equal(kv[1], seq[4])
+
+
+def test_station_on_first_node_fails_init():
+    """A station exactly on the grid's first x node triggers the reference's
+    SETBCS quirk (ierr = 1, fsm3d.f90:736-745): init fails instead of running
+    chains on u_nan tables."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem(n=20, seed=17)
+    p.sx = p.sx.copy()
+    p.sx[1] = p.x0
+    with pytest.raises(RuntimeError):
+        mcmc.Sampler(p, nchains=1)
