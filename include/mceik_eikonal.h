@@ -18,7 +18,10 @@ extern "C" {
  * job 1: initialise (ierr=1 if already initialised); job 2: solve (ierr=1 if
  * not initialised; ierr from SETBCS / FSM as the reference); other: finalise.
  * Computes on the GPU in fp64 with the reference's arithmetic: u is bitwise
- * equal to the reference's output.  slow, u: [nx*ny*nz], x fastest. */
+ * equal to the reference's output.  slow, u: [nx*ny*nz], x fastest.  Job 1
+ * allocates the device state (freed by the finalising call); one solve runs
+ * on the whole GPU (brick-level dataflow).  Any number of
+ * sources. */
 void eikonal3d_serial_driver(const int *job, const int *iverb, const int *maxit, const int *nsrc,
                              const int *nx, const int *ny, const int *nz, const double *tol,
                              const double *h, const double *x0, const double *y0, const double *z0,
@@ -32,6 +35,33 @@ void eikonal3d_serial_driver_sp(const int *job, const int *iverb, const int *max
                                 const double *h, const double *x0, const double *y0, const double *z0,
                                 const double *ts, const double *xs, const double *ys, const double *zs,
                                 const double *slow, double *u, int *ierr);
+
+/* Replaces the MPI variant EIKONAL3D_INITIALIZE / _SOLVE / _FINALIZE
+ * (fsm3d.f90:1583-1598, 1754-1769, 1891-1899), every argument by pointer.
+ * One GPU holds the whole grid: comm, ndivx/y/z and noverlap are accepted and
+ * unused.  The master passes the full arrays (n = nx*ny*nz) and receives u;
+ * a rank passing n < nx*ny*nz (the reference's callers use n = 1) returns at
+ * once with ierr = 0.  fp64 with the serial driver's arithmetic: u is the
+ * Gauss-Seidel fixed point of the reference (xfsm3d: max u = 1.4308203212738235). */
+void eikonal3d_initialize(const int *comm, const int *iverb, const int *nx, const int *ny, const int *nz,
+                          const int *ndivx, const int *ndivy, const int *ndivz, const int *noverlap,
+                          const int *maxit, const double *x0, const double *y0, const double *z0,
+                          const double *h, const double *tol, int *ierr);
+void eikonal3d_solve(const int *comm, const int *nsrc, const int *n, const double *ts, const double *xs,
+                     const double *ys, const double *zs, const double *slow, double *u, int *ierr);
+void eikonal3d_finalize(const int *comm, int *ierr);
+
+/* Replaces locate3d_gridsearch__double64 / __float64 (gridsearch.f90:382-540),
+ * the Fortran misfit variant (t0 weight 1/(var_i * sum var), logPDF weight
+ * sqrt(1/2)/var_i; SURVEY s.8a a12): same arguments by pointer, checks
+ * (ldgrd % 64, ngrd <= ldgrd, some unmasked observation, sum var != 0) and
+ * arithmetic order; host arrays, test [nobs][ldgrd]. */
+void locate3d_gridsearch__double64(const int *ldgrd, const int *ngrd, const int *nobs, const int *iwantOT,
+                                   const int *mask, const double *tobs, const double *varobs, const double *test,
+                                   double *logPDF, int *ierr);
+void locate3d_gridsearch__float64(const int *ldgrd, const int *ngrd, const int *nobs, const int *iwantOT,
+                                  const int *mask, const float *tobs, const float *varobs, const float *test,
+                                  float *logPDF, int *ierr);
 
 /* Replaces locate_l2_gridSearch__double64 (locate.c:923-1047): same
  * arguments, errors and results (bitwise); host arrays, computed on the GPU.

@@ -77,7 +77,9 @@ class McmcOpts(C.Structure):
 
 
 # every extern "C" symbol include/*.h declares
-EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "locate_l2_gridSearch__double64",
+EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_initialize", "eikonal3d_solve",
+           "eikonal3d_finalize", "locate3d_gridsearch__double64", "locate3d_gridsearch__float64",
+           "locate_l2_gridSearch__double64",
            "locate_l2_gridSearch__float64", "mceik_relocate",
            "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
@@ -99,6 +101,16 @@ def lib():
         f = getattr(L, name)
         f.restype = None
         f.argtypes = [pi] * 7 + [pd] * 5 + [C.c_void_p] * 6 + [pi]
+    L.eikonal3d_initialize.restype = None
+    L.eikonal3d_initialize.argtypes = [pi] * 10 + [pd] * 5 + [pi]
+    L.eikonal3d_solve.restype = None
+    L.eikonal3d_solve.argtypes = [pi] * 3 + [C.c_void_p] * 6 + [pi]
+    L.eikonal3d_finalize.restype = None
+    L.eikonal3d_finalize.argtypes = [pi, pi]
+    for name in ("locate3d_gridsearch__double64", "locate3d_gridsearch__float64"):
+        f = getattr(L, name)
+        f.restype = None
+        f.argtypes = [pi] * 4 + [C.c_void_p] * 5 + [pi]
     L.locate_l2_gridSearch__double64.restype = C.c_int
     L.locate_l2_gridSearch__double64.argtypes = [C.c_int] * 4 + [C.c_double] + [C.c_void_p] * 7
     L.mceik_fsm_workspace_bytes.restype = C.c_size_t

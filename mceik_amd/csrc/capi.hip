@@ -17,6 +17,7 @@
 #include "../../include/mceik.h"
 #include "fsm_common.h"
 #include "mcmc_common.h"
+#include "fsm_single.h"
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st);
 int fsm_occupancy(const FsmLaunch &L, int is_double);
@@ -30,6 +31,9 @@ hipError_t mcmc_accept(const McmcDev &D, int keep_slot, hipStream_t st);
 hipError_t l2_gridsearch_f32(int ldgrd, int ngrd, int nev, int iwantOT, float t0use, const int *ev_ptr,
                              const int *obs_row, const float *tc, const float *wt, const float *xnorm,
                              const float *test, float *t0, float *objfn, int negate, hipStream_t st);
+hipError_t gridsearch_f90(int is_double, int ldgrd, int ngrd, int nuse, int iwantOT, const int *row,
+                          const void *tob, const void *w0, const void *wl, const void *test, void *logpdf,
+                          hipStream_t st);
 hipError_t l2_gridsearch(int ldgrd, int ngrd, int nuse, int iwantOT, double t0use, const int *use,
                          const double *tc, const double *wt, double xnorm, const double *test,
                          double *t0, double *objfn, hipStream_t st);
@@ -267,10 +271,163 @@ extern "C" int mceik_memcpy(void *dst, const void *src, size_t bytes, int kind)
 }
 
 // ---------------------------------------------------------------------------
-// Drop-in serial driver (fsm3d.f90:1968-2052).  The reference keeps a level
-// structure between job 1 and job 3 (SAVE lstruct, linit); the GPU schedule
-// needs none, so only the init flag is kept, with the same error behaviour.
-static int g_serial_init[2] = {0, 0};
+// Drop-in single-solve entry points: the serial driver (fsm3d.f90:1968-2052)
+// and the MPI variant eikonal3d_initialize / _solve / _finalize
+// (fsm3d.f90:1583-1929).  One solve at a time runs on the whole GPU
+// (fsm_single.hip).  The reference's job-1 state (SAVE lstruct, linit,
+// fsm3d.f90:1985-1988) becomes the device state below: the brick level
+// order (MAKE_LEVEL_STRUCT at brick granularity) and every device buffer,
+// allocated at init and freed at finalize, so a solve call only copies the
+// model in, runs, and copies the field out.
+struct SingleState {
+    int init;
+    int nx, ny, nz, maxit_cap, nsrc_cap;
+    int is_double;
+    SingleLaunch L;
+    void *mem;                   // one allocation: fields, flags, tables
+    double *dense, *src;         // fp64 x-fastest staging [n], sources [nsrc][4]
+    int *ierr_bc;
+    int nwaves;
+    int bcfail;                  // the last solve stopped in SETBCS
+    hipStream_t st;
+    // MPI-variant parameters (eikonal3d_initialize)
+    int iverb, maxit;
+    double x0, y0, z0, h, tol;
+};
+static SingleState g_single[3];          // [0] serial fp32, [1] serial fp64, [2] MPI variant (fp64)
+
+static void single_free(SingleState &S)
+{
+    if (S.mem) hipFree(S.mem);
+    if (S.st) hipStreamDestroy(S.st);
+    const int keep = S.init;
+    memset(&S, 0, sizeof(S));
+    S.init = keep;
+}
+
+// Device buffers of a solve on nx x ny x nz (maxit iterations, nsrc sources).
+static int single_alloc(SingleState &S, int is_double, int nx, int ny, int nz, int maxit, int nsrc)
+{
+    if (S.mem && S.is_double == is_double && S.nx == nx && S.ny == ny && S.nz == nz && maxit <= S.maxit_cap &&
+        nsrc <= S.nsrc_cap)
+        return 0;
+    const int keep = S.init;
+    single_free(S);
+    S.init = keep;
+    if (nx < 1 || ny < 1 || nz < 1 || (long)nx * ny * nz >= (1L << 31)) return 1;
+    SingleLaunch &L = S.L;
+    L.nx = nx; L.ny = ny; L.nz = nz;
+    L.nbx = mceik_div_up(nx, 8); L.nby = mceik_div_up(ny, 8); L.nbz = mceik_div_up(nz, 8);
+    if (L.nbx > 1024 || L.nby > 1024 || L.nbz > 1024) return 1;
+    L.nxp = 8 * L.nbx; L.nyp = 8 * L.nby; L.nzp = 8 * L.nbz;
+    L.nb = L.nbx * L.nby * L.nbz;
+    if ((size_t)L.nxp * L.nyp * L.nzp * (is_double ? 8 : 4) >= ((size_t)1 << 31)) return 1;   // 32-bit offsets
+    const int mcap = maxit > 0 ? maxit : 1, scap = nsrc > 0 ? nsrc : 1;
+    const size_t es = is_double ? 8 : 4, np = (size_t)L.nxp * L.nyp * L.nzp, n = (size_t)nx * ny * nz;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    size_t off[12], o = 0;
+    off[0] = o; o += al(np * es);                      // u
+    off[1] = o; o += al(np * es);                      // u0
+    off[2] = o; o += al(np * es);                      // slow
+    off[3] = o; o += al(np);                           // bc
+    off[4] = o; o += al((size_t)L.nb * 4);             // border
+    off[5] = o; o += al((size_t)L.nb * 4);             // done
+    off[6] = o; o += al((size_t)(32 + mcap) * 4);      // ctl
+    off[7] = o; o += al((size_t)mcap * 8);             // arrive
+    off[8] = o; o += al((size_t)mcap * 4);             // ierr_it
+    off[9] = o; o += al(n * 8);                        // dense fp64 staging
+    off[10] = o; o += al((size_t)scap * 32);           // sources
+    off[11] = o; o += al(16);                          // SETBCS ierr
+    if (hipMalloc(&S.mem, o) != hipSuccess) { S.mem = nullptr; return 1; }
+    char *m = (char *)S.mem;
+    L.u = m + off[0]; L.u0 = m + off[1]; L.slow = m + off[2]; L.bc = (unsigned char *)(m + off[3]);
+    L.border = (const int *)(m + off[4]); L.done = (unsigned *)(m + off[5]); L.ctl = (unsigned *)(m + off[6]);
+    L.arrive = (unsigned long long *)(m + off[7]); L.ierr_it = (int *)(m + off[8]);
+    S.dense = (double *)(m + off[9]); S.src = (double *)(m + off[10]); S.ierr_bc = (int *)(m + off[11]);
+    L.bcerr = S.ierr_bc;
+    // brick level order in sweep coordinates (any order inside a level)
+    std::vector<int> ord;
+    ord.reserve(L.nb);
+    for (int lev = 0; lev <= L.nbx + L.nby + L.nbz - 3; lev++)
+        for (int bz = 0; bz < L.nbz; bz++)
+            for (int by = 0; by < L.nby; by++) {
+                const int bx = lev - bz - by;
+                if (bx >= 0 && bx < L.nbx) ord.push_back(bx | (by << 10) | (bz << 20));
+            }
+    if ((int)ord.size() != L.nb ||
+        hipMemcpy((void *)L.border, ord.data(), ord.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess) {
+        single_free(S);
+        return 1;
+    }
+    // persistent waves: every wave of the grid is resident (tasks are taken
+    // in dependency order, so a waiting wave only ever waits for running ones)
+    static const int wpc = [] { const char *e = getenv("MCEIK_SINGLE_WAVES_PER_CU"); return e ? atoi(e) : 2; }();
+    int occ = fsm_single_occupancy(is_double);
+    S.nwaves = device_cus() * std::max(1, std::min(wpc, occ));
+    S.is_double = is_double; S.nx = nx; S.ny = ny; S.nz = nz; S.maxit_cap = mcap; S.nsrc_cap = scap;
+    return 0;
+}
+
+// SETBCS + FSM of one model on the GPU; slow/u: host fp64 [nx*ny*nz].  Returns
+// the reference's ierr (1: SETBCS, fsm3d.f90:736-753; else the ierr of node
+// (1,1,1) in the last sweep, :78-82) or -1 on a device failure.
+static int single_solve(SingleState &S, int maxit, int nsrc, double tol, double h, double x0, double y0, double z0,
+                        const double *ts, const double *xs, const double *ys, const double *zs, const double *slow,
+                        double *u, int *niter_out)
+{
+    SingleLaunch &L = S.L;
+    const size_t n = (size_t)L.nx * L.ny * L.nz;
+    L.maxit = maxit; L.tol = tol; L.h = h; L.x0 = x0; L.y0 = y0; L.z0 = z0;
+    std::vector<double> src((size_t)nsrc * 4);
+    for (int k = 0; k < nsrc; k++) {
+        src[k * 4 + 0] = ts[k]; src[k * 4 + 1] = xs[k]; src[k * 4 + 2] = ys[k]; src[k * 4 + 3] = zs[k];
+    }
+    const int mcap = maxit > 0 ? maxit : 1;
+    std::vector<unsigned> ctl(32 + mcap);
+    std::vector<int> ierr_it(mcap);
+    int ierr_bc = 0;
+    hipStream_t st = S.st;
+    if (hipMemcpyAsync(S.dense, slow, n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(S.src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        fsm_single_pad(S.dense, (void *)L.slow, S.is_double, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
+        hipMemsetAsync(L.done, 0, (size_t)L.nb * 4, st) != hipSuccess ||
+        hipMemsetAsync(L.ctl, 0, (size_t)(32 + mcap) * 4, st) != hipSuccess ||
+        hipMemsetAsync(L.arrive, 0, (size_t)mcap * 8, st) != hipSuccess ||
+        hipMemsetAsync(L.ierr_it, 0, (size_t)mcap * 4, st) != hipSuccess ||
+        fsm_single_solve(L, S.is_double, S.src, nsrc, S.ierr_bc, S.nwaves, st) != hipSuccess ||
+        fsm_single_unpad(L.u, S.dense, S.is_double, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
+        hipMemcpyAsync(u, S.dense, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(ctl.data(), L.ctl, ctl.size() * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(ierr_it.data(), L.ierr_it, ierr_it.size() * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&ierr_bc, S.ierr_bc, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return -1;
+    if (ctl[1] != 0) {
+        std::vector<unsigned> done(L.nb);
+        std::vector<unsigned long long> arr(mcap);
+        hipMemcpy(done.data(), L.done, done.size() * 4, hipMemcpyDeviceToHost);
+        hipMemcpy(arr.data(), L.arrive, arr.size() * 8, hipMemcpyDeviceToHost);
+        unsigned dmin = ~0u, dmax = 0;
+        for (unsigned d : done) { dmin = std::min(dmin, d); dmax = std::max(dmax, d); }
+        fprintf(stderr, "mceik_hip: single-solve schedule timed out (code %u; waits timed out: deps %u, "
+                        "iteration %u; tasks taken %u, nb %d, done %u..%u, arrivals it0 %llu/%llu it1 %llu, "
+                        "decisions %u %u %u)\n", ctl[1], ctl[3], ctl[4], ctl[0], L.nb, dmin, dmax,
+                arr[0] & 0xffffffffull, arr[0] >> 32, mcap > 1 ? arr[1] & 0xffffffffull : 0ull, ctl[32],
+                mcap > 1 ? ctl[33] : 0u, mcap > 2 ? ctl[34] : 0u);
+        return -1;
+    }
+    S.bcfail = ierr_bc != 0;
+    if (ierr_bc) {
+        if (niter_out) *niter_out = 0;
+        return 1;
+    }
+    int niter = maxit > 0 ? maxit : 0;
+    for (int it = 0; it < maxit; it++)
+        if (ctl[32 + it] == 2) { niter = it + 1; break; }
+    if (niter_out) *niter_out = niter;
+    return niter > 0 ? ierr_it[niter - 1] : 0;
+}
 
 static void serial_driver(int is_double, const int *job, const int *iverb, const int *maxit,
                           const int *nsrc, const int *nx, const int *ny, const int *nz,
@@ -278,80 +435,48 @@ static void serial_driver(int is_double, const int *job, const int *iverb, const
                           const double *z0, const double *ts, const double *xs, const double *ys,
                           const double *zs, const double *slow, double *u, int *ierr)
 {
-    int &linit = g_serial_init[is_double];
+    SingleState &S = g_single[is_double];
     *ierr = 0;
     if (*job == 1) {
-        if (linit) { printf(" eikonal3d_serial_driver: Already initialized!\n"); *ierr = 1; return; }
+        if (S.init) { printf(" eikonal3d_serial_driver: Already initialized!\n"); *ierr = 1; return; }
         if (*iverb > 0) printf(" eikonal3d_serial_driver: Generating levels...\n");
-        linit = 1;
+        if (single_alloc(S, is_double, *nx, *ny, *nz, *maxit, *nsrc)) {
+            printf(" eikonal3d_serial_driver: Error generating level structure\n");
+            *ierr = 1;
+            return;
+        }
+        S.init = 1;
         return;
     }
     if (*job != 2) {
-        if (!linit) printf(" eikonal3d_serial_driver: Never initialized!\n");
-        linit = 0;
+        if (!S.init) printf(" eikonal3d_serial_driver: Never initialized!\n");
+        single_free(S);
+        S.init = 0;
         return;
     }
-    if (!linit) { printf(" eikonal3d_serial_driver: Solver not initalized!\n"); *ierr = 1; return; }
+    if (!S.init) { printf(" eikonal3d_serial_driver: Solver not initalized!\n"); *ierr = 1; return; }
     if (*nsrc < 1) {
         printf(" eikonal3d_serial_driver: nsrc must be >= 1\n");
         *ierr = 1;
         return;
     }
-    size_t n = (size_t)(*nx) * (*ny) * (*nz);
-    std::vector<double> src((size_t)(*nsrc) * 4);
-    for (int s = 0; s < *nsrc; s++) {
-        src[s * 4 + 0] = ts[s]; src[s * 4 + 1] = xs[s]; src[s * 4 + 2] = ys[s]; src[s * 4 + 3] = zs[s];
-    }
-    mceik_fsm_batch b;
-    memset(&b, 0, sizeof(b));
-    b.nx = *nx; b.ny = *ny; b.nz = *nz; b.h = *h; b.x0 = *x0; b.y0 = *y0; b.z0 = *z0;
-    b.maxit = *maxit; b.tol = *tol; b.precision = is_double ? 64 : 32;
-    b.nmodel = 1; b.nstat = 1; b.nsrc = *nsrc; b.slow_mode = 0; b.max_sweeps = -1;
-    size_t es = is_double ? 8 : 4;
-    void *d_slow = nullptr, *d_u = nullptr, *ws = nullptr;
-    double *d_src = nullptr;
-    int *d_ierr = nullptr;
-    hipError_t e = hipSuccess;
-    size_t wsb;
-    std::vector<float> h32;
-    auto fail = [&](const char *what) {
-        printf(" eikonal3d_serial_driver: %s failed (%s)\n", what, hipGetErrorString(e));
+    // a solve on another grid than job 1's (the reference's level structure
+    // would not match): reallocate rather than fail
+    if (single_alloc(S, is_double, *nx, *ny, *nz, *maxit, *nsrc)) {
+        printf(" eikonal3d_serial_driver: device allocation failed\n");
         *ierr = 1;
-    };
-    if ((e = hipMalloc(&d_slow, n * es)) != hipSuccess) { fail("hipMalloc"); goto done; }
-    if ((e = hipMalloc(&d_u, n * es)) != hipSuccess) { fail("hipMalloc"); goto done; }
-    if ((e = hipMalloc(&d_src, src.size() * 8)) != hipSuccess) { fail("hipMalloc"); goto done; }
-    if ((e = hipMalloc(&d_ierr, sizeof(int))) != hipSuccess) { fail("hipMalloc"); goto done; }
-    if (is_double) {
-        e = hipMemcpy(d_slow, slow, n * 8, hipMemcpyHostToDevice);
-    } else {
-        h32.resize(n);
-        for (size_t i = 0; i < n; i++) h32[i] = (float)slow[i];
-        e = hipMemcpy(d_slow, h32.data(), n * 4, hipMemcpyHostToDevice);
+        return;
     }
-    if (e != hipSuccess) { fail("hipMemcpy"); goto done; }
-    if ((e = hipMemcpy(d_src, src.data(), src.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) { fail("hipMemcpy"); goto done; }
-    b.src = d_src; b.slow = d_slow; b.u_out = d_u; b.ierr = d_ierr;
-    wsb = mceik_fsm_workspace_bytes(&b);
-    if ((e = hipMalloc(&ws, wsb)) != hipSuccess) { fail("hipMalloc"); goto done; }
-    if (*iverb > 0) printf(" eikonal3d_serial_driver: Solving...\n");
-    if (mceik_fsm_batch_solve(&b, ws, wsb, nullptr) != 0) { *ierr = 1; goto done; }
-    if ((e = hipDeviceSynchronize()) != hipSuccess) { fail("solve"); goto done; }
-    if (is_double) {
-        e = hipMemcpy(u, d_u, n * 8, hipMemcpyDeviceToHost);
-    } else {
-        h32.resize(n);
-        e = hipMemcpy(h32.data(), d_u, n * 4, hipMemcpyDeviceToHost);
-        for (size_t i = 0; i < n && e == hipSuccess; i++) u[i] = (double)h32[i];
+    if (*iverb > 0) printf(" eikonal3d_serial_driver: Setting boundary conditions...\n");
+    const int rc = single_solve(S, *maxit, *nsrc, *tol, *h, *x0, *y0, *z0, ts, xs, ys, zs, slow, u, nullptr);
+    if (rc < 0) {
+        printf(" eikonal3d_serial_driver: device failure\n");
+        *ierr = 1;
+        return;
     }
-    if (e != hipSuccess) { fail("hipMemcpy"); goto done; }
-    if ((e = hipMemcpy(ierr, d_ierr, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess) { fail("hipMemcpy"); goto done; }
-    if (*ierr != 0) {
-        if (*ierr == 1 && 0) {}
-        printf(" eikonal3d_serial_driver: Error solving eikonal equation\n");
-    }
-done:
-    hipFree(d_slow); hipFree(d_u); hipFree(d_src); hipFree(d_ierr); hipFree(ws);
+    *ierr = rc;
+    if (S.bcfail) printf(" eikonal3d_serial_driver: Error setting boundary conditions\n");
+    else if (rc != 0) printf(" eikonal3d_serial_driver: Error solving eikonal equation\n");
 }
 
 extern "C" void eikonal3d_serial_driver(const int *job, const int *iverb, const int *maxit, const int *nsrc,
@@ -370,6 +495,154 @@ extern "C" void eikonal3d_serial_driver_sp(const int *job, const int *iverb, con
                                            const double *slow, double *u, int *ierr)
 {
     serial_driver(0, job, iverb, maxit, nsrc, nx, ny, nz, tol, h, x0, y0, z0, ts, xs, ys, zs, slow, u, ierr);
+}
+
+// MPI variant (fsm3d.f90:1583-1929) on one GPU.  The reference decomposes the
+// grid over ndivx*ndivy*ndivz ranks of `comm` and gathers u on rank 0; here
+// the whole grid lives on the calling process's GPU, so the decomposition
+// arguments and `comm` are accepted and not used.  Collective semantics are
+// kept by the reference's own convention: the master passes the full arrays
+// (n = nx*ny*nz) and gets the travel times; every other rank passes n < nx*ny*nz
+// (the reference's callers use n = 1, fsm3d.f90:2102-2106) and returns at once
+// with ierr = 0.  Computes in fp64 with the serial driver's arithmetic, so u is
+// the Gauss-Seidel fixed point the reference's decomposed solve converges to
+// (xfsm3d: max u = 1.4308203212738235 from both).
+extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const int *nx, const int *ny, const int *nz,
+                                     const int *ndivx, const int *ndivy, const int *ndivz, const int *noverlap,
+                                     const int *maxit, const double *x0, const double *y0, const double *z0,
+                                     const double *h, const double *tol, int *ierr)
+{
+    (void)comm; (void)ndivx; (void)ndivy; (void)ndivz; (void)noverlap;
+    SingleState &S = g_single[2];
+    *ierr = 0;
+    if (*iverb > 0) printf(" eikonal3d_initialize: Broadcasting parameters...\n");
+    if (single_alloc(S, 1, *nx, *ny, *nz, *maxit, 1)) {
+        printf(" eikonal3d_initialize: Error making the device structures\n");
+        *ierr = 1;
+        return;
+    }
+    S.iverb = *iverb; S.maxit = *maxit; S.x0 = *x0; S.y0 = *y0; S.z0 = *z0; S.h = *h; S.tol = *tol;
+    S.init = 1;
+}
+
+extern "C" void eikonal3d_solve(const int *comm, const int *nsrc, const int *n, const double *ts, const double *xs,
+                                const double *ys, const double *zs, const double *slow, double *u, int *ierr)
+{
+    (void)comm;
+    SingleState &S = g_single[2];
+    *ierr = 0;
+    if (!S.init) {
+        printf(" eikonal3d_solve: solver not initialized\n");
+        *ierr = 1;
+        return;
+    }
+    if ((long)*n < (long)S.nx * S.ny * S.nz) return;          // not the master: nothing to hold
+    if (*nsrc < 1 || single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, *nsrc)) {
+        printf(" eikonal3d_solve: Error setting bcs\n");
+        *ierr = 1;
+        return;
+    }
+    if (S.iverb > 0) printf(" eikonal3d_solve: Setting boundary conditions...\n");
+    const int rc = single_solve(S, S.maxit, *nsrc, S.tol, S.h, S.x0, S.y0, S.z0, ts, xs, ys, zs, slow, u, nullptr);
+    if (S.bcfail) printf(" eikonal3d_solve: Error setting bcs\n");
+    else if (rc != 0) printf(" eikonal3d_solve: Error calling solver\n");
+    *ierr = rc < 0 ? 1 : rc;
+}
+
+extern "C" void eikonal3d_finalize(const int *comm, int *ierr)
+{
+    (void)comm;
+    single_free(g_single[2]);
+    g_single[2].init = 0;
+    *ierr = 0;
+}
+
+// ---------------------------------------------------------------------------
+// locate3d_gridsearch__double64 / __float64 drop-ins (gridsearch.f90:382-540).
+template <typename T>
+static void gridsearch_f90_dropin(const char *fcnm, const int *ldgrd, const int *ngrd, const int *nobs,
+                                  const int *iwantOT, const int *mask, const T *tobs, const T *varobs, const T *test,
+                                  T *logPDF, int *ierr)
+{
+    *ierr = 0;
+    if (*ldgrd % 64 != 0) {
+        printf(" %s: Require arrays be 64 byte aligned %d %d\n", fcnm, *ldgrd,
+               sizeof(T) == 8 ? (8 * *ldgrd) % 64 : *ldgrd % 64);
+        *ierr = 1;
+        return;
+    }
+    if (*ngrd > *ldgrd) {
+        printf(" %s: ngrd cannot be greater than ldgrd\n", fcnm);
+        *ierr = 1;
+        return;
+    }
+    long msum = 0;
+    T vsum = (T)0;
+    for (int i = 0; i < *nobs; i++) { msum += mask[i]; vsum = vsum + varobs[i]; }
+    if (msum == *nobs) {
+        printf(" %s: No observations\n", fcnm);
+        *ierr = 1;
+        return;
+    }
+    const T eps = sizeof(T) == 8 ? (T)DBL_EPSILON : (T)FLT_EPSILON;
+    if ((vsum < (T)0 ? -vsum : vsum) < eps) {
+        printf(" %s: Will be division by zero\n", fcnm);
+        *ierr = 1;
+        return;
+    }
+    T xnorm = (T)0;
+    for (int i = 0; i < *nobs; i++) if (mask[i] != 1) xnorm = xnorm + varobs[i];
+    const T one = (T)1, sqrt2i = one / (sizeof(T) == 8 ? (T)sqrt(2.0) : (T)sqrtf(2.0f));
+    std::vector<int> row;
+    std::vector<T> tob, w0, wl;
+    for (int i = 0; i < *nobs; i++) {
+        if (mask[i] == 1) continue;
+        row.push_back(i);
+        tob.push_back(tobs[i]);
+        w0.push_back(one / (varobs[i] * xnorm));
+        wl.push_back(sqrt2i / varobs[i]);
+    }
+    const int nuse = (int)row.size();
+    const size_t tb = (size_t)*ldgrd * *nobs * sizeof(T);
+    char *d = nullptr;
+    const size_t a = ((size_t)nuse * 16 + 255) & ~(size_t)255;
+    if (hipMalloc(&d, 4 * a + tb + (size_t)*ngrd * sizeof(T) + 64) != hipSuccess) {
+        printf(" %s: device allocation failed\n", fcnm);
+        *ierr = 1;
+        return;
+    }
+    int *d_row = (int *)d;
+    T *d_tob = (T *)(d + a), *d_w0 = (T *)(d + 2 * a), *d_wl = (T *)(d + 3 * a);
+    T *d_test = (T *)(d + 4 * a), *d_lp = (T *)(d + 4 * a + tb);
+    bool ok = hipMemcpy(d_row, row.data(), nuse * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_tob, tob.data(), nuse * sizeof(T), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_w0, w0.data(), nuse * sizeof(T), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_wl, wl.data(), nuse * sizeof(T), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_test, test, tb, hipMemcpyHostToDevice) == hipSuccess &&
+              gridsearch_f90(sizeof(T) == 8, *ldgrd, *ngrd, nuse, *iwantOT, d_row, d_tob, d_w0, d_wl, d_test, d_lp,
+                             nullptr) == hipSuccess &&
+              hipMemcpy(logPDF, d_lp, (size_t)*ngrd * sizeof(T), hipMemcpyDeviceToHost) == hipSuccess;
+    hipFree(d);
+    if (!ok) {
+        printf(" %s: device failure\n", fcnm);
+        *ierr = 1;
+    }
+}
+
+extern "C" void locate3d_gridsearch__double64(const int *ldgrd, const int *ngrd, const int *nobs, const int *iwantOT,
+                                              const int *mask, const double *tobs, const double *varobs,
+                                              const double *test, double *logPDF, int *ierr)
+{
+    gridsearch_f90_dropin<double>("locate3d_gridsearch_double64", ldgrd, ngrd, nobs, iwantOT, mask, tobs, varobs,
+                                  test, logPDF, ierr);
+}
+
+extern "C" void locate3d_gridsearch__float64(const int *ldgrd, const int *ngrd, const int *nobs, const int *iwantOT,
+                                             const int *mask, const float *tobs, const float *varobs,
+                                             const float *test, float *logPDF, int *ierr)
+{
+    gridsearch_f90_dropin<float>("locate3d_gridsearch_float64", ldgrd, ngrd, nobs, iwantOT, mask, tobs, varobs,
+                                 test, logPDF, ierr);
 }
 
 // ---------------------------------------------------------------------------

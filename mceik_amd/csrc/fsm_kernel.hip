@@ -19,53 +19,9 @@
 #include <stdint.h>
 
 #include "fsm_common.h"
+#include "fsm_update.h"
 
 namespace {
-
-template <typename R> struct Num;
-template <> struct Num<float> {
-    static __device__ __forceinline__ float unan() { return FLT_MAX; }
-    static __device__ __forceinline__ float sqrt_(float x) { return __builtin_sqrtf(x); }
-};
-template <> struct Num<double> {
-    static __device__ __forceinline__ double unan() { return DBL_MAX; }
-    static __device__ __forceinline__ double sqrt_(double x) { return __builtin_sqrt(x); }
-};
-
-// ---- the Godunov local solve ------------------------------------------------
-// fp64: the reference's literal SOLVE_HAMILTONIAN2D/3D (fsm3d.f90:624-693).
-// fp32: godunov_bl / godunov_v below, bitwise equal to oracle/fsm_impl.inc
-// STABLE_UPDATE (increments relative to a1, one square root per solve).
-__device__ __forceinline__ double godunov(double a, double b, double c, double f, int &ierr)
-{
-    const double UN = DBL_MAX;
-    double a1, a2, a3;
-    bool lab = !(a > b), lac = !(a > c), lbc = !(b > c);
-    if (lab && lac) { a1 = a; a2 = lbc ? b : c; a3 = lbc ? c : b; }
-    else if (!lab && lbc) { a1 = b; a2 = lac ? a : c; a3 = lac ? c : a; }
-    else { a1 = c; a2 = lab ? a : b; a3 = lab ? b : a; }
-    ierr = 0;
-    if (a1 == UN) return UN;
-    double x = a1 + f;
-    if (!(x > a2)) return x;
-    double amb = a1 - a2;
-    if (__builtin_fabs(amb) < f) {
-        double arg = (2.0 * f) * f - amb * amb;
-        x = 0.5 * ((a1 + a2) + __builtin_sqrt(arg));
-    } else {
-        x = (a1 < a2 ? a1 : a2) + f;
-    }
-    if (!(x > a3)) return x;
-    double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
-    double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
-    double disc = qb * qb - 4.0 * qc;
-    if (disc < 0.0) ierr = 1;
-    x = 0.5 * (-qb + __builtin_sqrt(disc));
-    if (x < 0.0) ierr = 2;
-    if (x < UN) return x;
-    ierr = 3;
-    return UN;
-}
 
 // ---- buffer resources: 32-bit offsets, out-of-range reads return 0 and
 // out-of-range writes are dropped, so predicated memory ops need no branches.
@@ -158,59 +114,6 @@ __device__ __forceinline__ double bperm(int addr, double v)
     unsigned lo = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)u);
     unsigned hi = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(u >> 32));
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
-// Correctly rounded sqrt for normal positive x (LLVM's expansion without the
-// denormal rescale and zero/inf fix-up).  Used only where the radicand that
-// is finally selected is provably a normal float: on the MCMC path f = h*s >=
-// h/vmax (checked on the host) and the selected radicand exceeds f^2 (2D:
-// 2f^2 - d2^2 with d2 < f; 3D: 3f^2 - d2^2 - (d3^2 + (d3-d2)^2) with both
-// terms < f^2).
-__device__ __forceinline__ float sqrt_normal(float x)
-{
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float dn = __builtin_bit_cast(float, __builtin_bit_cast(int, s) - 1);
-    const float up = __builtin_bit_cast(float, __builtin_bit_cast(int, s) + 1);
-    const float edn = __builtin_fmaf(-dn, s, x);
-    const float eup = __builtin_fmaf(-up, s, x);
-    const float t = edn <= 0.0f ? dn : s;
-    return eup > 0.0f ? up : t;
-}
-
-// Branchless fp32 Godunov update, values and ierr identical to the twin
-// (oracle/fsm_impl.inc STABLE_UPDATE): 1D if f <= d2, else the 2D root unless
-// d3^2 + (d3 - d2)^2 < f^2 (the 2D root would exceed d3), then the 3D root;
-// only the selected radicand is square-rooted.
-template <bool FAST>
-__device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, int &ierr)
-{
-    const float UN = FLT_MAX;
-    const float a1 = fminf(fminf(a, b), c);
-    const float a3 = fmaxf(fmaxf(a, b), c);
-    const float a2 = __builtin_amdgcn_fmed3f(a, b, c);
-    const float d2 = a2 - a1, d3 = a3 - a1;
-    const float ff = f * f, e = d3 - d2;
-    const float d22 = d2 * d2, d33 = d3 * d3;
-    const bool two = (d33 + e * e) >= ff;
-    const float r2 = (ff + ff) - d22;
-    const float sm = d2 + d3;
-    const float q = (d22 + d33) - ff;
-    const float disc = sm * sm - 3.0f * q;
-    const float rad = two ? r2 : disc;
-    const float s = FAST ? sqrt_normal(rad) : __builtin_sqrtf(rad);
-    const float y23 = two ? 0.5f * (d2 + s) : (sm + s) * (1.0f / 3.0f);
-    const bool one = !(f > d2);
-    const float y = one ? f : y23;
-    const float x = a1 + y;
-    const bool ok = x < UN;
-    const bool nan_in = a1 == UN;
-    ierr = nan_in ? 0 : (!ok ? 3 : ((!one && !two && disc < 0.0f) ? 1 : 0));
-    return (nan_in || !ok) ? UN : x;
-}
-template <bool FAST>
-__device__ __forceinline__ double godunov_bl(double a, double b, double c, double f, int &ierr)
-{
-    return godunov(a, b, c, f, ierr);   // fp64: the reference's literal form
 }
 
 // Column order inside a brick: the tile perimeter first -- rows ly = 0 and
@@ -833,17 +736,6 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> 
     }
     asm volatile("" ::: "memory");
 }
-
-// min of two travel times.  Values in the field are never NaN or -0 (every
-// update is clamped to FLT_MAX, sources are ts + d*s >= +0), so for fp32 the
-// unsigned order of the bit patterns is the float order: v_min_u32 needs no
-// IEEE canonicalisation of its inputs (v_min_f32 does).
-__device__ __forceinline__ float fmin_(float a, float b)
-{
-    const unsigned ia = __builtin_bit_cast(unsigned, a), ib = __builtin_bit_cast(unsigned, b);
-    return __builtin_bit_cast(float, __builtin_elementwise_min(ia, ib));
-}
-__device__ __forceinline__ double fmin_(double a, double b) { return __builtin_fmin(a, b); }
 
 // Godunov update without the error code (fast path): fp32 values identical to
 // godunov_bl (a1 == UN or an overflowing / NaN candidate gives UN either way).

@@ -195,7 +195,46 @@ __global__ void l2_gridsearch_f32_kernel(int ldgrd, int ngrd, int iwantOT, float
     }
 }
 
+// Fortran misfit variant (gridsearch.f90:176-540): per grid point the t0 stack
+// (LOCATE3D_STACK_T0_*, weight 1/(var_i * sum var)) then the logPDF stack
+// (LOCATE3D_STACK_LOGPDF_*, weight sqrt(1/2)/var_i), observations in order.
+// Host-compacted arrays: row[j] of test, tob[j], w0[j] = 1/(var*xnorm),
+// wl[j] = sqrt2i/var, computed in T exactly as the Fortran does.
+template <typename T>
+__global__ void gridsearch_f90_kernel(int ldgrd, int ngrd, int nuse, int iwantOT, const int *row, const T *tob,
+                                      const T *w0, const T *wl, const T *test, T *logpdf)
+{
+    for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < ngrd; g += gridDim.x * blockDim.x) {
+        T t0 = (T)0;
+        if (iwantOT == 1)
+            for (int j = 0; j < nuse; j++) t0 = t0 + w0[j] * (tob[j] - test[(size_t)ldgrd * row[j] + g]);
+        T lp = (T)0;
+        for (int j = 0; j < nuse; j++) {
+            const T res = wl[j] * (tob[j] - (test[(size_t)ldgrd * row[j] + g] + t0));
+            lp = lp + res * res;
+        }
+        logpdf[g] = lp;
+    }
+}
+
 }  // namespace
+
+hipError_t gridsearch_f90(int is_double, int ldgrd, int ngrd, int nuse, int iwantOT, const int *row,
+                          const void *tob, const void *w0, const void *wl, const void *test, void *logpdf,
+                          hipStream_t st)
+{
+    int bx = (ngrd + 255) / 256;
+    if (bx > 4096) bx = 4096;
+    if (is_double)
+        hipLaunchKernelGGL(gridsearch_f90_kernel<double>, dim3(bx), dim3(256), 0, st, ldgrd, ngrd, nuse, iwantOT,
+                           row, (const double *)tob, (const double *)w0, (const double *)wl, (const double *)test,
+                           (double *)logpdf);
+    else
+        hipLaunchKernelGGL(gridsearch_f90_kernel<float>, dim3(bx), dim3(256), 0, st, ldgrd, ngrd, nuse, iwantOT,
+                           row, (const float *)tob, (const float *)w0, (const float *)wl, (const float *)test,
+                           (float *)logpdf);
+    return hipGetLastError();
+}
 
 hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st)
 {

@@ -49,6 +49,52 @@ def eikonal3d_serial_driver(job, iverb, maxit, nsrc, nx, ny, nz, tol, h, x0, y0,
     return ierr.value
 
 
+def eikonal3d_initialize(iverb, nx, ny, nz, ndivx, ndivy, ndivz, noverlap, maxit, x0, y0, z0, h, tol, comm=0):
+    """EIKONAL3D_INITIALIZE (fsm3d.f90:1583-1598); returns ierr.  One GPU holds
+    the whole grid: comm and the decomposition are accepted, not used."""
+    L = _lib.lib()
+    ierr = C.c_int(0)
+    L.eikonal3d_initialize(_ip(comm), _ip(iverb), _ip(nx), _ip(ny), _ip(nz), _ip(ndivx), _ip(ndivy), _ip(ndivz),
+                           _ip(noverlap), _ip(maxit), _dp(x0), _dp(y0), _dp(z0), _dp(h), _dp(tol), C.byref(ierr))
+    return ierr.value
+
+
+def eikonal3d_solve(nsrc, n, ts, xs, ys, zs, slow, u, comm=0):
+    """EIKONAL3D_SOLVE (fsm3d.f90:1754-1889): the master passes n = nx*ny*nz and
+    gets u (float64, filled in place); n < nx*ny*nz is a non-master rank."""
+    L = _lib.lib()
+    keep = [_arr(np.atleast_1d(v)) for v in (ts, xs, ys, zs)]
+    sl, slp = _arr(slow)
+    if u.dtype != np.float64 or not u.flags.c_contiguous or u.size < n or sl.size < n:
+        raise ValueError("slow/u must hold n float64 values (u C-contiguous)")
+    ierr = C.c_int(0)
+    L.eikonal3d_solve(_ip(comm), _ip(nsrc), _ip(n), keep[0][1], keep[1][1], keep[2][1], keep[3][1], slp,
+                      u.ctypes.data_as(C.c_void_p), C.byref(ierr))
+    return ierr.value
+
+
+def eikonal3d_finalize(comm=0):
+    L = _lib.lib()
+    ierr = C.c_int(0)
+    L.eikonal3d_finalize(_ip(comm), C.byref(ierr))
+    return ierr.value
+
+
+def locate3d_gridsearch(ldgrd, ngrd, nobs, iwantOT, mask, tobs, varobs, test, logpdf):
+    """locate3d_gridsearch__double64 / __float64 (gridsearch.f90:382-540) by the
+    dtype of `logpdf` (float64 / float32); test [nobs*ldgrd]; returns ierr."""
+    L = _lib.lib()
+    dt = logpdf.dtype
+    f = L.locate3d_gridsearch__double64 if dt == np.float64 else L.locate3d_gridsearch__float64
+    m = np.ascontiguousarray(mask, dtype=np.int32)
+    to, va, te = (np.ascontiguousarray(a, dtype=dt) for a in (tobs, varobs, test))
+    ierr = C.c_int(0)
+    f(_ip(ldgrd), _ip(ngrd), _ip(nobs), _ip(iwantOT), m.ctypes.data_as(C.c_void_p), to.ctypes.data_as(C.c_void_p),
+      va.ctypes.data_as(C.c_void_p), te.ctypes.data_as(C.c_void_p), logpdf.ctypes.data_as(C.c_void_p),
+      C.byref(ierr))
+    return ierr.value
+
+
 def locate_l2_gridsearch(ldgrd, ngrd, nobs, iwantOT, t0use, mask, tobs, tcorr, varobs, test, t0, objfn):
     """locate_l2_gridSearch__double64 (locate.c:923-1047) on the GPU; returns ierr.
     t0/objfn/test must be 64-byte aligned float64 arrays, as the reference requires."""

@@ -35,5 +35,8 @@ $F -O2 -fopenmp -o xfsm3d mod/mpimod.o mod/module.o mod/mpiutils.o mod/fsm3d.o \
 : > inc/lapacke_utils.h
 gcc -O2 -fPIC -shared -I inc -I/opt/conda/include '-DMIN(a,b)=((a)<(b)?(a):(b))' '-DMAX(a,b)=((a)>(b)?(a):(b))' \
     -Dmain=locate_c_unused_main "$R/locate.c" -o liblocate_ref.so -lm 2> inc/locate.warn || { cat inc/locate.warn; exit 1; }
-$F -O2 -module-dir mod "$R/gridsearch.f90" -o xgridsearch
+$F -O2 -module-dir mod "$R/gridsearch.f90" -o xgridsearch 2> mod/gridsearch.warn
+# the same file's BIND(C) locate3d_gridsearch__double64/__float64 as a shared
+# object (flang's main() lives in its runtime, so the PROGRAM unit links inert)
+$F -O2 -fPIC -shared -module-dir mod "$R/gridsearch.f90" -o libgridsearch_ref.so 2>> mod/gridsearch.warn
 echo "build_ref: built $(ls "$OUT" | tr '\n' ' ')"

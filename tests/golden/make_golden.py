@@ -126,6 +126,60 @@ def make_fsm(ref):
         print(f"fsm_{name}: ierr={ierr} umax={u.max()!r}")
 
 
+def make_gridsearch():
+    """gridsearch.f90:382-540 (locate3d_gridsearch__double64 / __float64, the
+    Fortran misfit variant) from oracle/_ref/libgridsearch_ref.so: straight-ray
+    tables on a 31 x 27 x 9 grid, 12 stations, unequal variances, one masked
+    observation and one mask value other than 0/1 (counts as used:
+    gridsearch.f90:432 tests mask /= 1), with and without the origin time."""
+    lib = C.CDLL(os.path.join(REF, "libgridsearch_ref.so"))
+    nx, ny, nz, nobs, dx = 31, 27, 9, 12, 1.0e3
+    ngrd = nx * ny * nz
+    ldgrd = ngrd + 64 - ngrd % 64
+    rng = np.random.default_rng(2024)
+    rec = rng.random((nobs, 3)) * (np.array([nx, ny, nz]) - 1) * dx
+    src = np.array([13.0, 19.0, 4.0]) * dx
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    pts = np.stack([i.ravel(), j.ravel(), k.ravel()], 1) * dx
+    test = np.zeros(nobs * ldgrd)
+    for o in range(nobs):
+        test[o * ldgrd:o * ldgrd + ngrd] = np.sqrt(((pts - rec[o]) ** 2).sum(1)) / 5.0e3
+    tobs = np.sqrt(((rec - src) ** 2).sum(1)) / 5.0e3 + 4.0 + rng.normal(0.0, 0.01, nobs)
+    varobs = rng.uniform(0.5, 2.0, nobs)
+    mask = np.zeros(nobs, np.int32)
+    mask[3] = 1
+    mask[7] = 2
+    ip = lambda v: C.byref(C.c_int(v))
+    out = dict(ldgrd=ldgrd, ngrd=ngrd, nobs=nobs, test=test, tobs=tobs, varobs=varobs, mask=mask)
+    for prec, name in ((64, "locate3d_gridsearch__double64"), (32, "locate3d_gridsearch__float64")):
+        dt = np.float64 if prec == 64 else np.float32
+        f = getattr(lib, name)
+        for iw in (1, 0):
+            lp = np.zeros(ngrd, dt)
+            ierr = C.c_int(-1)
+            t, to, va = (np.ascontiguousarray(a, dtype=dt) for a in (test, tobs, varobs))
+            f(ip(ldgrd), ip(ngrd), ip(nobs), ip(iw), _ptr(mask), _ptr(to), _ptr(va), _ptr(t), _ptr(lp),
+              C.byref(ierr))
+            assert ierr.value == 0
+            out[f"logpdf{prec}_ot{iw}"] = lp
+            print(f"gridsearch f{prec} iwantOT={iw}: argmin={int(np.argmin(lp))} true={(4 * ny + 19) * nx + 13}")
+        # the reference's checks (ierr = 1): ldgrd % 64, ngrd > ldgrd, every observation masked
+        for tag, args in (("ld", (ldgrd + 1, ngrd)), ("ng", (ldgrd, ldgrd + 64))):
+            ierr = C.c_int(-1)
+            lp = np.zeros(ldgrd + 64, dt)
+            t, to, va = (np.ascontiguousarray(a, dtype=dt) for a in (np.zeros(nobs * (ldgrd + 64)), tobs, varobs))
+            f(ip(args[0]), ip(args[1]), ip(nobs), ip(1), _ptr(mask), _ptr(to), _ptr(va), _ptr(t), _ptr(lp),
+              C.byref(ierr))
+            out[f"ierr{prec}_{tag}"] = ierr.value
+        allm = np.ones(nobs, np.int32)
+        ierr = C.c_int(-1)
+        lp = np.zeros(ngrd, dt)
+        t, to, va = (np.ascontiguousarray(a, dtype=dt) for a in (test, tobs, varobs))
+        f(ip(ldgrd), ip(ngrd), ip(nobs), ip(1), _ptr(allm), _ptr(to), _ptr(va), _ptr(t), _ptr(lp), C.byref(ierr))
+        out[f"ierr{prec}_allmasked"] = ierr.value
+    np.savez_compressed(os.path.join(HERE, "gridsearch_f90.npz"), **out)
+
+
 def make_locate():
     """locate.c main()-style inputs (locate.c:108-164) on a smaller grid,
     generated with the reference's own makeTest/makeObs and glibc rand()."""
@@ -201,3 +255,4 @@ if __name__ == "__main__":
         sys.exit("build the reference first: oracle/build_ref.sh")
     make_fsm(RefFSM())
     make_locate()
+    make_gridsearch()

@@ -1,0 +1,128 @@
+"""The drop-in entry points a single-call user links (fsm3d.f90 / gridsearch.f90
+BIND(C) names) on the GPU:
+
+* eikonal3d_serial_driver (fp64) and _sp now run ONE solve on the whole GPU
+  (fsm_single.hip brick-level dataflow): bitwise the reference's golden
+  fields (test_gpu_fsm.py) and here bitwise the fp64 oracle / fp32 twin on
+  multi-source, ragged and repeated calls, with the device state kept from
+  job 1 to job 3;
+* eikonal3d_initialize / _solve / _finalize from a C caller (tests/c) in the
+  flow of the reference's xfsm3d program: its known answer
+  max u = 1.4308203212738235;
+* locate3d_gridsearch__double64 / __float64 bitwise the compiled
+  gridsearch.f90 (tests/golden/gridsearch_f90.npz), with its error checks.
+"""
+import os
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _hetero(nx, ny, nz):
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    return 3000.0 + 4000.0 * k / (nz - 1) + 500.0 * np.sin(0.3 * i) * np.cos(0.25 * j) * np.sin(0.2 * k)
+
+
+def _serial(nx, ny, nz, slow, src, maxit=50, tol=1e-8, h=100.0, precision=64, reps=1):
+    from mceik_amd.eikonal import eikonal3d_serial_driver
+    s = np.atleast_2d(src)
+    u = np.zeros(nx * ny * nz)
+    args = (maxit, len(s), nx, ny, nz, tol, h, 0.0, 0.0, 0.0, s[:, 0], s[:, 1], s[:, 2], s[:, 3], slow, u)
+    assert eikonal3d_serial_driver(1, 0, *args, precision=precision) == 0
+    times, outs = [], []
+    for _ in range(reps):
+        t = time.perf_counter()
+        ierr = eikonal3d_serial_driver(2, 0, *args, precision=precision)
+        times.append(time.perf_counter() - t)
+        outs.append((u.copy(), ierr))
+    eikonal3d_serial_driver(3, 0, *args, precision=precision)
+    return outs, times
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_serial_driver_many_sources_ragged(precision):
+    """12 sources (no source-count limit), a ragged 37 x 29 x 21 grid (partial
+    bricks in x, y and z), called twice on the kept device state."""
+    _dev()
+    nx, ny, nz = 37, 29, 21
+    rng = np.random.default_rng(8)
+    slow = (1.0 / (2500.0 + 3500.0 * rng.random(nx * ny * nz)))
+    src = np.stack([rng.uniform(0.02, 0.3, 12), rng.uniform(100, 3500, 12), rng.uniform(100, 2700, 12),
+                    rng.uniform(100, 1900, 12)], 1)
+    outs, _ = _serial(nx, ny, nz, slow, src, precision=precision, reps=2)
+    dt = np.float64 if precision == 64 else np.float32
+    ref, ierr, _ = O.eikonal_solve(nx, ny, nz, slow.astype(dt), 100.0, src, dtype=dt)
+    for u, e in outs:
+        assert e == ierr == 0
+        if precision == 64:
+            assert np.array_equal(u.view(np.uint64), ref.view(np.uint64))
+        else:
+            assert np.array_equal(u.astype(np.float32).view(np.uint32), ref.view(np.uint32))
+
+
+def test_serial_driver_128cube_time_and_bitwise():
+    """One 128^3 heterogeneous fp64 call, bitwise the fp64 oracle (the
+    reference's arithmetic); wall time of warm calls printed (one call with the
+    one-wave-per-solve kernel took ~0.8 s; the CPU reference 0.7-4 s)."""
+    _dev()
+    n = 128
+    slow = (1.0 / _hetero(n, n, n)).ravel()
+    src = np.array([0.0, 6437.0, 6389.0, 12700.0])
+    outs, times = _serial(n, n, n, slow, src, reps=3)
+    ref, ierr, it = O.eikonal_solve(n, n, n, slow, 100.0, src)
+    for u, e in outs:
+        assert e == ierr
+        assert np.array_equal(u.view(np.uint64), ref.view(np.uint64))
+    print(f"\nserial_driver 128^3 fp64: {it} iterations, call times {[round(t, 4) for t in times]} s")
+    assert min(times) < 1.0
+
+
+def test_mpi_variant_from_c_caller(tmp_path):
+    _dev()
+    exe = str(tmp_path / "xfsm3d_gpu")
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c", "xfsm3d_gpu.c"),
+                    "-L", os.path.join(ROOT, "mceik_amd"), "-lmceik_hip", "-Wl,-rpath," + os.path.join(ROOT, "mceik_amd"),
+                    "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = {ln.split()[0]: ln.split() for ln in out.stdout.splitlines() if ln.strip()}
+    assert float(lines["mpi_variant"][4]) == 1.4308203212738235
+    assert float(lines["mpi_variant"][2]) == 0.0
+    assert lines["non_master"][2] == "0" and float(lines["non_master"][4]) == -1.0
+    assert float(lines["serial_driver"][4]) == 1.4308203212738235
+
+
+@pytest.mark.parametrize("prec", [64, 32])
+def test_locate3d_gridsearch_bitwise_vs_reference(prec):
+    from mceik_amd.eikonal import locate3d_gridsearch
+    _dev()
+    g = dict(np.load(os.path.join(GOLD, "gridsearch_f90.npz"), allow_pickle=False))
+    ld, ng, no = int(g["ldgrd"]), int(g["ngrd"]), int(g["nobs"])
+    dt = np.float64 if prec == 64 else np.float32
+    ut = np.uint64 if prec == 64 else np.uint32
+    for iw in (1, 0):
+        lp = np.zeros(ng, dt)
+        assert locate3d_gridsearch(ld, ng, no, iw, g["mask"], g["tobs"], g["varobs"], g["test"], lp) == 0
+        assert np.array_equal(lp.view(ut), g[f"logpdf{prec}_ot{iw}"].view(ut)), iw
+    lp = np.zeros(ld + 64, dt)
+    big = np.zeros(no * (ld + 64))
+    assert locate3d_gridsearch(ld + 1, ng, no, 1, g["mask"], g["tobs"], g["varobs"], big, lp) == g[f"ierr{prec}_ld"] == 1
+    assert locate3d_gridsearch(ld, ld + 64, no, 1, g["mask"], g["tobs"], g["varobs"], big, lp) == g[f"ierr{prec}_ng"] == 1
+    assert locate3d_gridsearch(ld, ng, no, 1, np.ones(no), g["tobs"], g["varobs"], g["test"], lp[:ng]) == \
+        g[f"ierr{prec}_allmasked"] == 1
