@@ -97,6 +97,10 @@ typedef struct mceik_relocate_batch {
     float *t0;                  /* device [nev][ldgrd] or NULL               */
     float *out;                 /* device [nev][ldgrd]                       */
     int log_pdf;
+    int nrows;                  /* rows of `tables` (> every obs_row) and nobs = ev_ptr[nev] on the
+                                   host: single-pass kernel (each table value read once per launch,
+                                   LDS-staged); 0 = unknown, two passes per event from HBM */
+    int nobs;
 } mceik_relocate_batch;
 int mceik_relocate(const mceik_relocate_batch *b, void *stream);
 

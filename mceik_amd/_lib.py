@@ -32,7 +32,7 @@ class RelocateBatch(C.Structure):
     _fields_ = [("ldgrd", C.c_int), ("ngrd", C.c_int), ("nev", C.c_int), ("iwantOT", C.c_int),
                 ("t0use", C.c_float), ("tables", C.c_void_p), ("ev_ptr", C.c_void_p), ("obs_row", C.c_void_p),
                 ("tc", C.c_void_p), ("wt", C.c_void_p), ("xnorm", C.c_void_p), ("t0", C.c_void_p),
-                ("out", C.c_void_p), ("log_pdf", C.c_int)]
+                ("out", C.c_void_p), ("log_pdf", C.c_int), ("nrows", C.c_int), ("nobs", C.c_int)]
 
 
 class McmcParms(C.Structure):

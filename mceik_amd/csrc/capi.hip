@@ -31,6 +31,10 @@ hipError_t mcmc_accept(const McmcDev &D, int keep_slot, hipStream_t st);
 hipError_t l2_gridsearch_f32(int ldgrd, int ngrd, int nev, int iwantOT, float t0use, const int *ev_ptr,
                              const int *obs_row, const float *tc, const float *wt, const float *xnorm,
                              const float *test, float *t0, float *objfn, int negate, hipStream_t st);
+size_t relocate_lds_bytes(int nrows, int nobs, int nev);
+hipError_t relocate_lds(int ldgrd, int ngrd, int nrows, int nev, int nobs, int iwantOT, float t0use,
+                        const int *ev_ptr, const int *obs_row, const float *tc, const float *wt, const float *xnorm,
+                        const float *test, float *t0, float *objfn, int negate, hipStream_t st);
 hipError_t gridsearch_f90(int is_double, int ldgrd, int ngrd, int nuse, int iwantOT, const int *row,
                           const void *tob, const void *w0, const void *wl, const void *test, void *logpdf,
                           hipStream_t st);
@@ -779,6 +783,10 @@ extern "C" int mceik_relocate(const mceik_relocate_batch *b, void *stream)
         fprintf(stderr, "mceik_relocate: invalid batch description\n");
         return 1;
     }
+    if (b->nrows > 0 && b->nobs >= 0 && relocate_lds_bytes(b->nrows, b->nobs, b->nev) <= 64 * 1024)
+        return relocate_lds(b->ldgrd, b->ngrd, b->nrows, b->nev, b->nobs, b->iwantOT, b->t0use, b->ev_ptr, b->obs_row,
+                            b->tc, b->wt, b->xnorm, b->tables, b->t0, b->out, b->log_pdf ? 1 : 0,
+                            (hipStream_t)stream) != hipSuccess;
     return l2_gridsearch_f32(b->ldgrd, b->ngrd, b->nev, b->iwantOT, b->t0use, b->ev_ptr, b->obs_row, b->tc, b->wt,
                              b->xnorm, b->tables, b->t0, b->out, b->log_pdf ? 1 : 0, (hipStream_t)stream) != hipSuccess;
 }

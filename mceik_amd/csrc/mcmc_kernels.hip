@@ -195,6 +195,96 @@ __global__ void l2_gridsearch_f32_kernel(int ldgrd, int ngrd, int iwantOT, float
     }
 }
 
+// Single-pass relocation (SURVEY s.8f row 2): a block stages the travel-time
+// tables of its TG grid points -- every row, once -- in LDS, and each thread
+// then evaluates ALL events at its grid point from its own LDS column, so a
+// table value leaves HBM once per launch instead of twice per event that
+// observes it.  The per-observation weights wt/xnorm and wt*sqrt(1/2) are
+// formed once per block (the same fp32 operations as l2_gridsearch_f32_kernel,
+// so every output is bitwise the same) into per-event groups aligned to 4, read
+// back as 16-B uniform (broadcast) LDS loads by the 4-way unrolled pair loops.
+// LDS: [nrows][TG] tables | per event 4-aligned (tc, w0, w1, row*TG) | offsets.
+template <int TG>
+__global__ __launch_bounds__(TG) void relocate_lds_kernel(int ldgrd, int ngrd, int nrows, int nev, int nobs,
+                                                          int iwantOT, float t0use, const int *ev_ptr,
+                                                          const int *obs_row, const float *tc, const float *wt,
+                                                          const float *xnorm, const float *test, float *t0,
+                                                          float *objfn, int negate)
+{
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *tile = sm;                                   // [nrows][TG]
+    const int cap = (nobs + 3 * nev + 3) & ~3;          // obs slots with per-event padding to 4
+    float *stc = sm + (size_t)nrows * TG, *sw0 = stc + cap, *sw1 = sw0 + cap;
+    int *srow = (int *)(sw1 + cap), *soff = srow + cap;    // soff [nev + 1]
+    const float sqrt2i = 0.7071067811865475f;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        int o = 0;
+        for (int e = 0; e < nev; e++) {
+            soff[e] = o;
+            o += (ev_ptr[e + 1] - ev_ptr[e] + 3) & ~3;
+        }
+        soff[nev] = o;
+    }
+    __syncthreads();
+    for (int e = 0; e < nev; e++) {
+        const float xn = xnorm[e];
+        const int j0 = ev_ptr[e], base = soff[e] - j0;
+        for (int j = j0 + tid; j < ev_ptr[e + 1]; j += TG) {
+            stc[base + j] = tc[j];
+            sw0[base + j] = wt[j] / xn;
+            sw1[base + j] = wt[j] * sqrt2i;
+            srow[base + j] = obs_row[j] * TG;
+        }
+    }
+    const int g = blockIdx.x * TG + tid;
+    const bool in = g < ngrd;
+    for (int r = 0; r < nrows; r++) tile[r * TG + tid] = in ? test[(size_t)ldgrd * r + g] : 0.0f;
+    __syncthreads();
+    if (!in) return;
+    const float *col = tile + tid;
+    for (int e = 0; e < nev; e++) {
+        const int b = soff[e], n = ev_ptr[e + 1] - ev_ptr[e], n4 = n & ~3;
+        float t = 0.0f;
+        if (iwantOT == 1) {
+            for (int k = 0; k < n4; k += 4) {
+                const f4 c4 = *(const f4 *)(stc + b + k), w4 = *(const f4 *)(sw0 + b + k);
+                const i4 r4 = *(const i4 *)(srow + b + k);
+                const float te0 = col[r4.x], te1 = col[r4.y], te2 = col[r4.z], te3 = col[r4.w];
+                t = t + w4.x * (c4.x - te0);
+                t = t + w4.y * (c4.y - te1);
+                t = t + w4.z * (c4.z - te2);
+                t = t + w4.w * (c4.w - te3);
+            }
+            for (int k = n4; k < n; k++) t = t + sw0[b + k] * (stc[b + k] - col[srow[b + k]]);
+        } else {
+            t = t0use;
+        }
+        float o = 0.0f;
+        for (int k = 0; k < n4; k += 4) {
+            const f4 c4 = *(const f4 *)(stc + b + k), w4 = *(const f4 *)(sw1 + b + k);
+            const i4 r4 = *(const i4 *)(srow + b + k);
+            const float te0 = col[r4.x], te1 = col[r4.y], te2 = col[r4.z], te3 = col[r4.w];
+            float res = w4.x * (c4.x - (te0 + t));
+            o = o + res * res;
+            res = w4.y * (c4.y - (te1 + t));
+            o = o + res * res;
+            res = w4.z * (c4.z - (te2 + t));
+            o = o + res * res;
+            res = w4.w * (c4.w - (te3 + t));
+            o = o + res * res;
+        }
+        for (int k = n4; k < n; k++) {
+            const float res = sw1[b + k] * (stc[b + k] - (col[srow[b + k]] + t));
+            o = o + res * res;
+        }
+        if (t0) t0[(size_t)e * ldgrd + g] = t;
+        objfn[(size_t)e * ldgrd + g] = negate ? -o : o;
+    }
+}
+
 // Fortran misfit variant (gridsearch.f90:176-540): per grid point the t0 stack
 // (LOCATE3D_STACK_T0_*, weight 1/(var_i * sum var)) then the logPDF stack
 // (LOCATE3D_STACK_LOGPDF_*, weight sqrt(1/2)/var_i), observations in order.
@@ -264,6 +354,23 @@ hipError_t l2_gridsearch(int ldgrd, int ngrd, int nuse, int iwantOT, double t0us
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(l2_gridsearch_kernel, dim3(blocks), dim3(256), 0, st, ldgrd, ngrd, nuse, iwantOT,
                        t0use, use, tc, wt, xnorm, test, t0, objfn);
+    return hipGetLastError();
+}
+
+#define RELOC_TG 256
+size_t relocate_lds_bytes(int nrows, int nobs, int nev)
+{
+    return (size_t)nrows * RELOC_TG * 4 + (size_t)((nobs + 3 * nev + 3) & ~3) * 16 + (size_t)(nev + 1) * 4;
+}
+
+hipError_t relocate_lds(int ldgrd, int ngrd, int nrows, int nev, int nobs, int iwantOT, float t0use,
+                        const int *ev_ptr, const int *obs_row, const float *tc, const float *wt, const float *xnorm,
+                        const float *test, float *t0, float *objfn, int negate, hipStream_t st)
+{
+    const size_t lds = relocate_lds_bytes(nrows, nobs, nev);
+    hipLaunchKernelGGL(relocate_lds_kernel<RELOC_TG>, dim3((ngrd + RELOC_TG - 1) / RELOC_TG), dim3(RELOC_TG), lds, st,
+                       ldgrd, ngrd, nrows, nev, nobs, iwantOT, t0use, ev_ptr, obs_row, tc, wt, xnorm, test, t0, objfn,
+                       negate);
     return hipGetLastError();
 }
 

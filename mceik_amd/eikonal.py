@@ -121,7 +121,8 @@ def locate_l2_gridsearch_f32(ldgrd, ngrd, nobs, iwantOT, t0use, mask, tobs, tcor
                                            p(m), p(to), p(tc), p(va), p(test), p(t0), p(objfn))
 
 
-def relocate(tables, events, ldgrd=None, iwantOT=1, t0use=0.0, log_pdf=True, stream=0):
+def relocate(tables, events, ldgrd=None, iwantOT=1, t0use=0.0, log_pdf=True, stream=0, single_pass=True,
+             want_t0=True):
     """Relocation grid search (SURVEY s.8f row 2) of many events against one
     model's travel-time tables, one GPU launch (mceik_relocate).
 
@@ -166,10 +167,12 @@ def relocate(tables, events, ldgrd=None, iwantOT=1, t0use=0.0, log_pdf=True, str
     b.ngrd = min(b.ngrd, ld)
     b.tables, b.ev_ptr, b.obs_row = tables.data_ptr(), d_ptr.data_ptr(), d_rows.data_ptr()
     b.tc, b.wt, b.xnorm = d_tc.data_ptr(), d_wt.data_ptr(), d_xn.data_ptr()
-    b.t0, b.out, b.log_pdf = t0.data_ptr(), out.data_ptr(), 1 if log_pdf else 0
+    b.t0, b.out, b.log_pdf = (t0.data_ptr() if want_t0 else None), out.data_ptr(), 1 if log_pdf else 0
+    if single_pass:
+        b.nrows, b.nobs = int(nrows), len(rows)
     if L.mceik_relocate(C.byref(b), C.c_void_p(stream)) != 0:
         raise RuntimeError("mceik_relocate failed")
-    return out, t0
+    return out, (t0 if want_t0 else None)
 
 
 def aligned_empty(n, dtype=np.float64, align=64):

@@ -296,7 +296,8 @@ def test_locate_l2_f32_gpu_bitwise_vs_reference():
                                     test, t0, obj) == 1
 
 
-def test_relocate_batch_matches_reference_per_event():
+@pytest.mark.parametrize("single_pass", [True, False], ids=["lds_single_pass", "two_pass"])
+def test_relocate_batch_matches_reference_per_event(single_pass):
     """Batched relocation (all events against shared tables, one launch) equals
     the reference fp32 L2 grid search event by event (oracle restatement,
     itself pinned to locate.c by the golden test)."""
@@ -312,7 +313,7 @@ def test_relocate_batch_matches_reference_per_event():
         mask = (rng.random(rows.size) < 0.2).astype(np.int32)
         events.append(dict(rows=rows, tobs=g["tobs"][rows] + np.float32(0.3 * e), varobs=g["varobs"][rows],
                            tcorr=g["tcorr"][rows], mask=mask))
-    out, t0 = relocate(tables, events, log_pdf=True)
+    out, t0 = relocate(tables, events, log_pdf=True, single_pass=single_pass)
     out = out.cpu().numpy(); t0 = t0.cpu().numpy()
     for e, ev in enumerate(events):
         sub_test = g["test"].reshape(no, ld)[ev["rows"]].ravel()
@@ -321,3 +322,21 @@ def test_relocate_batch_matches_reference_per_event():
         assert ierr == 0
         assert np.array_equal(t0[e, :ng].view(np.uint32), rt0.view(np.uint32))
         assert np.array_equal((-out[e, :ng]).view(np.uint32), robj.view(np.uint32))
+
+
+def test_relocate_single_pass_c3_catalogue():
+    """C3-sized relocation: 32 station tables on the 128^3 grid, 32 events x 32
+    P picks; the single-pass LDS kernel == the two-pass kernel bitwise."""
+    from mceik_amd.eikonal import relocate
+    dev = _dev()
+    n, nst, nev = 128, 32, 32
+    ngrd = n ** 3
+    g = torch.Generator(device=dev).manual_seed(3)
+    tables = torch.rand((nst, ngrd), generator=g, device=dev) * 4.0
+    rng = np.random.default_rng(7)
+    events = [dict(rows=np.arange(nst), tobs=rng.uniform(1.0, 5.0, nst).astype(np.float32),
+                   varobs=rng.uniform(0.5, 2.0, nst).astype(np.float32)) for _ in range(nev)]
+    a, ta = relocate(tables, events, log_pdf=True, single_pass=True)
+    b, tb = relocate(tables, events, log_pdf=True, single_pass=False)
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    assert torch.equal(ta.view(torch.int32), tb.view(torch.int32))
