@@ -136,6 +136,10 @@ typedef struct mceik_fsm_batch {
     int max_waves;              /* cap on the resident solve waves (0 = occupancy x CUs); with fewer
                                    waves than solves each wave runs several solves in its reused
                                    scratch field (the production path at C2/C3) */
+    unsigned long long *traffic;/* device [8] += requested global-memory bytes by category (own segment
+                                   loads, halo loads, z-upwind loads, own stores, u0 stores, cell loads,
+                                   convergence-check loads, init fill + table gather); counted only by
+                                   an accounting build (-DMCEIK_TRAFFIC), else untouched; or NULL */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */

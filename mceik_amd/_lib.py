@@ -24,7 +24,7 @@ class FsmBatch(C.Structure):
                 ("u_out", C.c_void_p), ("niter", C.c_void_p), ("ierr", C.c_void_p),
                 ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
                 ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p),
-                ("max_waves", C.c_int)]
+                ("max_waves", C.c_int), ("traffic", C.c_void_p)]
 
 
 class RelocateBatch(C.Structure):

@@ -114,6 +114,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.solve_order = b->solve_order;
     L.solve_clock = b->solve_clock;
     L.max_waves = b->max_waves;
+    L.traffic = b->traffic;
 }
 
 static int g_device_cus = 0;
@@ -1011,7 +1012,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     rc |= dalloc(s, &d_tt, (size_t)nch * nstat * nev);
     rc |= dalloc(s, &d_niter, (size_t)nch * nstat);
     rc |= dalloc(s, &s->d_ierr, (size_t)nch * nstat);
-    rc |= dalloc(s, &s->d_iters, 4);          // [0] iterations, [1..3] visit_stats
+    rc |= dalloc(s, &s->d_iters, 4 + MCEIK_TRAFFIC_N);   // [0] iterations, [1..3] visit_stats, [4..] traffic
     if (s->max_samples) {
         rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncell);
         rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
@@ -1031,6 +1032,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
     b.visit_stats = s->d_iters + 1;
+    b.traffic = s->d_iters + 4;
     b.max_waves = o->max_waves > 0 ? o->max_waves : 0;
     // f = h/v stays a normal float: the short correctly rounded sqrt (fp32 only)
     b.fast_sqrt = b.precision == 32 && parms->dx / (double)o->vmax >= 1e-12 ? 1 : 0;
@@ -1079,7 +1081,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
                     dmax * 1e-5, busy / (nch * nstat) * 1e-5, 100.0 * busy / ((double)nw * (double)(t1 - t0)));
         }
     }
-    hipMemset(s->d_iters, 0, 4 * sizeof(unsigned long long));
+    hipMemset(s->d_iters, 0, (4 + MCEIK_TRAFFIC_N) * sizeof(unsigned long long));
     *out = s;
     return 0;
 }
@@ -1168,7 +1170,7 @@ extern "C" int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *log
         HIPCHK(hipMemcpy(D.logl, logl, (size_t)D.nchains * 8, hipMemcpyHostToDevice));
     } else {
         // one forward of the restored models (not timed, not counted in the FSM stats)
-        unsigned long long keep[4];
+        unsigned long long keep[4 + MCEIK_TRAFFIC_N];
         HIPCHK(hipMemcpy(keep, s->d_iters, sizeof(keep), hipMemcpyDeviceToHost));
         if (mcmc_forward(s, false)) return -1;
         HIPCHK(mcmc_init_loglik(D, s->stream));
@@ -1230,8 +1232,19 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
         if (fold_launch(s, s->ev_folded)) return -1;
         s->ev_folded++;
     }
-    unsigned long long it[4] = {0, 0, 0, 0};
+    unsigned long long it[4 + MCEIK_TRAFFIC_N] = {0};
     HIPCHK(hipMemcpy(it, s->d_iters, sizeof(it), hipMemcpyDeviceToHost));
+    {   // accounting build: requested bytes per launch by category
+        unsigned long long tsum = 0;
+        for (int k = 0; k < MCEIK_TRAFFIC_N; k++) tsum += it[4 + k];
+        if (tsum && s->nlaunch) {
+            static const char *nm[MCEIK_TRAFFIC_N] = {"own_load", "halo_load", "zup_load", "own_store",
+                                                      "u0_store", "cell_load", "verify_load", "init_gather"};
+            fprintf(stderr, "mceik traffic (requested bytes per FSM launch, %lld launches):", s->nlaunch);
+            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) fprintf(stderr, " %s=%.6e", nm[k], (double)it[4 + k] / s->nlaunch);
+            fprintf(stderr, " total=%.6e\n", (double)tsum / s->nlaunch);
+        }
+    }
     if (fsm_ms) *fsm_ms = s->fsm_ms;
     if (nlaunch) *nlaunch = s->nlaunch;
     if (iters) *iters = it[0];
@@ -1240,7 +1253,7 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
         s->fsm_ms = 0.0;
         s->nlaunch = 0;
         s->ev_folded = 0;
-        HIPCHK(hipMemset(s->d_iters, 0, 4 * sizeof(unsigned long long)));
+        HIPCHK(hipMemset(s->d_iters, 0, (4 + MCEIK_TRAFFIC_N) * sizeof(unsigned long long)));
     }
     return 0;
 }

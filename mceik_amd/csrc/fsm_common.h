@@ -50,9 +50,21 @@ struct FsmLaunch {
     const int *solve_order;      // queue slot -> solve id, or null (slot = solve)
     unsigned long long *solve_clock;  // [nsolve][2] realtime at solve start / end, or null
     int max_waves;               // host only: cap on resident waves (0 = occupancy x CUs)
+    unsigned long long *traffic; // [MCEIK_TRAFFIC_N] requested bytes by category (MCEIK_TRAFFIC builds), or null
 };
 
 static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
+
+// Debug / accounting counters in LDS: [0..3] visit statistics; MCEIK_TRAFFIC
+// builds add [8..15], the requested global-memory bytes of the wave's current
+// sweep by category (flushed to FsmLaunch.traffic after every sweep).
+#ifdef MCEIK_TRAFFIC
+#define MCEIK_SCRATCH_BYTES 64
+#else
+#define MCEIK_SCRATCH_BYTES 32
+#endif
+#define MCEIK_TRAFFIC_N 8       // categories: own load, halo load, z-upwind load, own store, u0 store,
+                                // cell-cache load, verify loads (u + u0), init fill + BC + table gather
 
 // LDS of one solve wave (byte offsets, shared by host and device):
 //  0 BC boxes [nsrc][6] int (EIKONAL3D_SETBCS, fsm3d.f90:762-840; no source limit beyond LDS) | 1 cell cache [nr][ccb] float (cached mode) |
@@ -63,8 +75,35 @@ static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 #define MCEIK_CC_MAX 256         // cell-cache floats per position, upper bound
 #define MCEIK_SMEM_ARRAYS 12
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
+// The compile-time-kb cell-cache kernel (fsm_kernel.hip variant 8, the C3
+// sampler instance) uses a FIXED layout: every array base is a constant, so
+// LDS addresses fold into instruction offsets instead of occupying SGPRs
+// (the kernel runs at the SGPR limit).  Runtime-sized arrays (tile order,
+// BC boxes) come last; the block tables are sized for MCEIK_MAX_BLOCKS.
+#define FSMF_NR (2 + (16 + MCEIK_KB - 1) / MCEIK_KB)
+#define FSMF_CINFO 0
+#define FSMF_HALO (FSMF_CINFO + FSMF_NR * 64 * 16)
+#define FSMF_CC (FSMF_HALO + 256 * 4)
+#define FSMF_RING (FSMF_CC + FSMF_NR * 64 * 4)
+#define FSMF_SCRATCH (FSMF_RING + 64)
+#define FSMF_LASTPROC (FSMF_SCRATCH + MCEIK_SCRATCH_BYTES)
+#define FSMF_LASTCHG (FSMF_LASTPROC + MCEIK_MAX_BLOCKS * 4)
+#define FSMF_U0EP (FSMF_LASTCHG + MCEIK_MAX_BLOCKS * 4)
+#define FSMF_ORDER (FSMF_U0EP + MCEIK_MAX_BLOCKS * 2)
+static inline __host__ __device__ bool fsm_fixed_layout(const FsmLaunch &L, size_t es)
+{
+    return es == 4 && L.slow_mode != 0 && L.cell_cache && L.fast_sqrt && L.nrz == 4 && L.ccb <= 64 &&
+           L.kb == MCEIK_KB && L.nr == FSMF_NR && L.nblocks <= MCEIK_MAX_BLOCKS;
+}
 static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, size_t es, size_t *off)
 {
+    if (fsm_fixed_layout(L, es)) {
+        off[11] = FSMF_CINFO; off[9] = FSMF_HALO; off[10] = FSMF_HALO + 128 * 4; off[1] = FSMF_CC;
+        off[6] = FSMF_RING; off[7] = FSMF_SCRATCH; off[3] = FSMF_LASTPROC; off[4] = FSMF_LASTCHG;
+        off[5] = FSMF_U0EP; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;          // sf: unused (cells cached)
+        off[0] = FSMF_ORDER + mceik_align16((size_t)L.ntiles * 4);
+        return off[0] + mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
+    }
     const bool cached = L.slow_mode != 0 && L.cell_cache;
     const size_t nt = (size_t)L.ntiles, nb = (size_t)L.nblocks, nr = (size_t)L.nr;
     size_t o = 0;
@@ -75,7 +114,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[4] = o; o += mceik_align16(nb * 4);
     off[5] = o; o += mceik_align16(nb * 2);
     off[6] = o; o += mceik_align16(nr * 8);
-    off[7] = o; o += 32;
+    off[7] = o; o += MCEIK_SCRATCH_BYTES;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 128 * es;
     off[10] = o; o += 128 * es;

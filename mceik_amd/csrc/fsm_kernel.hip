@@ -200,11 +200,17 @@ struct Smem {
     R *halo;                     // staged halos [32 halo columns][8 z] (halo_col)
 };
 
-template <typename R>
+template <typename R, bool FIXED>
 __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *base)
 {
     size_t off[MCEIK_SMEM_ARRAYS];
-    fsm_smem_layout(L, sizeof(R), off);
+    if (FIXED) {         // fsm_fixed_layout(): constants (the host checked the predicate)
+        off[11] = FSMF_CINFO; off[9] = FSMF_HALO; off[1] = FSMF_CC; off[6] = FSMF_RING; off[7] = FSMF_SCRATCH;
+        off[3] = FSMF_LASTPROC; off[4] = FSMF_LASTCHG; off[5] = FSMF_U0EP; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;
+        off[0] = FSMF_ORDER + mceik_align16((size_t)L.ntiles * 4);
+    } else {
+        fsm_smem_layout(L, sizeof(R), off);
+    }
     Smem<R> S;
     S.box = reinterpret_cast<int *>(base + off[0]);
     S.cc = reinterpret_cast<float *>(base + off[1]);
@@ -219,6 +225,35 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     S.cinfo = reinterpret_cast<u4v *>(base + off[11]);
     return S;
 }
+
+// Traffic accounting (MCEIK_TRAFFIC builds): lane 0 adds bytes x (lanes where
+// pred holds) to the wave's LDS counter of category k.
+#ifdef MCEIK_TRAFFIC
+#define TRAF(S, k, pred, bytes)                                                                         \
+    do {                                                                                                \
+        const unsigned n_ = (unsigned)__builtin_popcountll(__ballot(pred));                             \
+        if (threadIdx.x == 0) (S).scratch[8 + (k)] += (int)(n_ * (unsigned)(bytes));                     \
+    } while (0)
+#define TRAFU(S, k, bytes)                                                                              \
+    do {                                                                                                \
+        if (threadIdx.x == 0) (S).scratch[8 + (k)] += (int)(bytes);                                     \
+    } while (0)
+// flush the wave's counters to the launch totals (after every sweep / solve)
+#define TRAF_FLUSH(L, S)                                                                                \
+    do {                                                                                                \
+        asm volatile("" ::: "memory");                                                                  \
+        if (threadIdx.x == 0 && (L).traffic)                                                            \
+            for (int k_ = 0; k_ < MCEIK_TRAFFIC_N; k_++) {                                              \
+                atomicAdd((L).traffic + k_, (unsigned long long)(unsigned)(S).scratch[8 + k_]);         \
+                (S).scratch[8 + k_] = 0;                                                                \
+            }                                                                                           \
+        asm volatile("" ::: "memory");                                                                  \
+    } while (0)
+#else
+#define TRAF(S, k, pred, bytes) do { } while (0)
+#define TRAFU(S, k, bytes) do { } while (0)
+#define TRAF_FLUSH(L, S) do { } while (0)
+#endif
 
 // Position of a lane in the stream of one sweep: stream position sp, its ring
 // slot ri = sp mod nr, and the step zbs (0..kb-1) inside the position,
@@ -997,6 +1032,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
         if (SLOWMODE == 2 && e >= 0) {
             cc_issue<CCR>(L, kb, sr, e, ccv, ccsize);
+            TRAFU(S, 5, ccsize * 4);
             cc_write<R, CCR>(L, S.cc, dri, ccv, ccsize, (float)L.h);
         }
         ndecided = pos + 1;
@@ -1014,14 +1050,26 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
     Pos pe;                              // the halo's edge lane position (vb+2 in the loop)
     pos_init(pe, -hd, kb, nr);
-    bload4(ur, halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]), hq);
+    {
+        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]);
+        bload4(ur, ho, hq);
+        TRAF(S, 1, ho != OOB, 4 * sizeof(R));
+    }
     zc = bload1(ur, b0.zh, R());
+    TRAF(S, 0, b0.seg != OOB, 8 * sizeof(R));
+    TRAF(S, 2, b0.zh != OOB, sizeof(R));
     pos_adv(p3, kb, nr);
     BInfo b1 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
     bload8(ur, b1.seg, n);
     pos_adv(pe, kb, nr);
-    bload4(ur, halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]), hn);   // halos of vb+1
+    {
+        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]);
+        bload4(ur, ho, hn);   // halos of vb+1
+        TRAF(S, 1, ho != OOB, 4 * sizeof(R));
+    }
     zn = bload1(ur, b1.zh, R());
+    TRAF(S, 0, b1.seg != OOB, 8 * sizeof(R));
+    TRAF(S, 2, b1.zh != OOB, sizeof(R));
     BInfo b2;
     if (AH == 3) {
         pos_adv(p3, kb, nr);
@@ -1067,10 +1115,19 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #endif
     int cc_pend = -1;                // ring slot whose cell loads (ccv) are written next step
     int B = 0;
-    auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
-        // ---- stream decision for the position lane (0,0) prefetches next
-        bool ccfill = false;
-        int ccri = 0;
+    // MCEIK_BOTTOM_EXIT: the stream decision for step B is made at the end of
+    // step B-1 (after its write-back, so it reads the same block clocks) and
+    // the loop tests its exit at the bottom: one path around the loop, so the
+    // loop-carried registers need no phi copies on a second edge
+#ifndef MCEIK_BOTTOM_EXIT
+#define MCEIK_BOTTOM_EXIT 1
+#endif
+    bool ccfill = false;
+    int ccri = 0;
+    auto decide_step = [&]() __attribute__((always_inline)) {
+        // ---- stream decision for the position lane (0,0) prefetches in step B
+        ccfill = false;
+        ccri = 0;
         if (ph == 0 && nstream == 0x7fffffff) {
             const int pos = ndecided;
             int zh;
@@ -1081,6 +1138,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
                 if (SLOWMODE == 2 && e >= 0) {
                     cc_issue<CCR>(L, kb, sr, e, ccv, ccsize);
+                    TRAFU(S, 5, ccsize * 4);
                     ccfill = true;
                     ccri = dri;
                 }
@@ -1088,7 +1146,15 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (++dri == nr) dri = 0;
             }
         }
-        if (nstream != 0x7fffffff && B >= nstream * kb + 14) return false;
+    };
+    auto more = [&]() __attribute__((always_inline)) -> bool {
+        return !(nstream != 0x7fffffff && B >= nstream * kb + 14);
+    };
+    auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
+        if (!MCEIK_BOTTOM_EXIT) {
+            decide_step();
+            if (!more()) return false;
+        }
         // ---- prefetch: own segment and halos of vb+AH (consumed at the end
         // of this step, before its stores; halos staged to LDS at the end of
         // the next), slowness of vb+1 (modes 0/1)
@@ -1109,7 +1175,13 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 bload8(ur, b3.seg, q);
             zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
         }
-        bload4(ur, halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, cie), hn);
+        {
+            const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, cie);
+            bload4(ur, ho, hn);
+            TRAF(S, 1, ho != OOB, 4 * sizeof(R));
+            TRAF(S, 0, b3.seg != OOB, 8 * sizeof(R));
+            TRAF(S, 2, b3.zh != OOB, sizeof(R));
+        }
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
 
         // ---- the 8 z-slots of the current brick
@@ -1177,11 +1249,13 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 pair_store(ur, b0.seg, changed, reinterpret_cast<const float (&)[8]>(r));
             else
                 bstore8(ur, changed ? b0.seg : OOB, r);
+            TRAF(S, 3, changed, 8 * sizeof(R));
         }
         if (!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) {      // a block's first visit in the iteration
             R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
             const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
             if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
+            TRAF(S, 4, st0, 8 * sizeof(R));
         }
         if (changed) S.lastchg[b0.bid] = clock0 + b0.clk;   // lanes of one block write the same value
         asm volatile("" ::: "memory");
@@ -1203,9 +1277,26 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
         if (++ph == kb) ph = 0;
         B++;
+        if (MCEIK_BOTTOM_EXIT) {
+            decide_step();
+            return more();
+        }
         return true;
     };
-    if (ROT) {
+    if (MCEIK_BOTTOM_EXIT) {
+        decide_step();
+        if (more()) {
+            if (ROT) {
+                for (;;) {
+                    if (!step(c, n, hq, hn)) break;
+                    if (!step(n, c, hn, hq)) break;
+                }
+            } else {
+                do {
+                } while (step(c, n, hq, hn));
+            }
+        }
+    } else if (ROT) {
         for (;;) {
             if (!step(c, n, hq, hn)) break;
             if (!step(n, c, hn, hq)) break;
@@ -1241,6 +1332,7 @@ __device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R
                 R u[8], v0[8];
                 bload8(ur, seg, u);
                 bload8(u0r, seg, v0);
+                TRAF(S, 6, x < L.nx && y < L.ny, 16 * sizeof(R));
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     R dl = v0[i] - u[i];
@@ -1362,7 +1454,7 @@ template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Smem<R> S = smem_bind<R>(L, smem);
+    const Smem<R> S = smem_bind<R, KB == MCEIK_KB && sizeof(R) == 4 && SLOWMODE == 2>(L, smem);
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
     build_order(L, S.order);
@@ -1398,6 +1490,10 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             S.u0ep[t] = 0;
         }
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
+#ifdef MCEIK_TRAFFIC
+        if (lane == 0)
+            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) S.scratch[8 + k] = 0;
+#endif
         unsigned nchg = 0;
         BcBoxes bc;
         bc.box = S.box;
@@ -1445,6 +1541,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
 #endif
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    TRAF_FLUSH(L, S);
                 }
                 iters = it + 1;
                 if (sweeps_left > 0 || L.max_sweeps < 0) {
@@ -1481,6 +1578,8 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             if (L.niter) L.niter[solve] = iters;
             if (L.ierr) L.ierr[solve] = ierr;
         }
+        TRAFU(S, 7, (unsigned)(L.field_elems * sizeof(R)) + (L.ttab ? (unsigned)L.nev * (4u + 64u) : 0u));
+        TRAF_FLUSH(L, S);
         if (L.ttab) {
             for (int e = lane; e < L.nev; e += 64) {
                 int node = L.ev_node[e];
@@ -1536,6 +1635,7 @@ template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 static hipError_t launch_fsm(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     size_t lds = fsm_lds_bytes(L, sizeof(R));
+    if (KB == MCEIK_KB && sizeof(R) == 4 && SLOWMODE == 2 && !fsm_fixed_layout(L, 4)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fsm_solve_kernel<R, SLOWMODE, FAST, ZSH, CCR, KB>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
 }
