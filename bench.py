@@ -130,7 +130,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-cores", type=int, default=0)
     ap.add_argument("--cpu-rounds", type=int, default=CPU_ROUNDS)
-    ap.add_argument("--sigma", type=float, default=1e-3, help="pick noise (s); varObs = sigma^2")
+    ap.add_argument("--sigma", type=float, default=5e-4, help="pick noise (s); varObs = sigma^2")
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     args = ap.parse_args()
 
