@@ -162,6 +162,10 @@ static int batch_waves(const FsmLaunch &L, int is_double)
     long w = (long)per_cu * device_cus();
     if (L.max_waves > 0 && w > L.max_waves) w = L.max_waves;
     if (w > L.nsolve) w = L.nsolve;
+    static const bool report = getenv("MCEIK_LAUNCH_REPORT") != nullptr;
+    if (report)
+        fprintf(stderr, "mceik fsm launch: %d waves/CU (occupancy), %ld resident waves, %zu B LDS per wave\n", per_cu,
+                w, fsm_lds_bytes(L, is_double ? 8 : 4));
     return (int)(w < 1 ? 1 : w);
 }
 

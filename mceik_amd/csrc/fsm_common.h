@@ -9,7 +9,9 @@
 #define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
 #define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
 #define MCEIK_KB 4               // bricks per z-block (stream position) when the block tables fit in LDS
+#ifndef MCEIK_MAX_BLOCKS
 #define MCEIK_MAX_BLOCKS 1024    // per-block clocks in LDS: at most this many z-blocks per field
+#endif
 #ifndef MCEIK_AHEAD
 #define MCEIK_AHEAD 2            // own segments are loaded this many macro steps ahead (2 or 3;
                                  // 3 measured 2.8% slower at C3: more visits from the longer in-flight window)
@@ -69,11 +71,14 @@ static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 // LDS of one solve wave (byte offsets, shared by host and device):
 //  0 BC boxes [nsrc][6] int (EIKONAL3D_SETBCS, fsm3d.f90:762-840; no source limit beyond LDS) | 1 cell cache [nr][ccb] float (cached mode) |
 //  2 diagonal tile order int [ntiles] | 3 lastproc int [nblocks] | 4 lastchg int [nblocks] |
-//  5 u0 epoch u16 [nblocks] | 6 stream entries int [nr] + block ids int [nr] | 7 run scratch int [8] |
-//  8 staged f [8][64] R (uncached) | 9+10 halos [32 columns][8] R (two halves of 128 R) |
-//  11 column info [nr][64] uint4
+//  5 (unused: a block's first visit in an iteration is lastproc < the iteration's first clock) |
+//  6 stream entries int [nr] + block ids int [nr] | 7 run scratch int [8] | 8 staged f [8][64] R (uncached) |
+//  9 neighbour rows XR, 10 neighbour rows XN: [2 halves][80 rows][4] R each -- row l < 64 holds lane l's
+//    8 z values (XR: its results of the last step, XN: its next brick), rows 64..79 the tile's halo columns |
+//  11 column info [nr][64] uint2 {own column offset, flags | tz | cell-cache base}
 #define MCEIK_CC_MAX 256         // cell-cache floats per position, upper bound
 #define MCEIK_SMEM_ARRAYS 12
+#define MCEIK_XROWS 80           // neighbour-row array: 64 lanes + 8 x-halo + 8 y-halo rows
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
 // The compile-time-kb cell-cache kernel (fsm_kernel.hip variant 8, the C3
 // sampler instance) uses a FIXED layout: every array base is a constant, so
@@ -82,14 +87,14 @@ static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 1
 // BC boxes) come last; the block tables are sized for MCEIK_MAX_BLOCKS.
 #define FSMF_NR (2 + (16 + MCEIK_KB - 1) / MCEIK_KB)
 #define FSMF_CINFO 0
-#define FSMF_HALO (FSMF_CINFO + FSMF_NR * 64 * 16)
-#define FSMF_CC (FSMF_HALO + 256 * 4)
+#define FSMF_XR (FSMF_CINFO + FSMF_NR * 64 * 8)
+#define FSMF_XN (FSMF_XR + 2 * MCEIK_XROWS * 16)
+#define FSMF_CC (FSMF_XN + 2 * MCEIK_XROWS * 16)
 #define FSMF_RING (FSMF_CC + FSMF_NR * 64 * 4)
 #define FSMF_SCRATCH (FSMF_RING + 64)
 #define FSMF_LASTPROC (FSMF_SCRATCH + MCEIK_SCRATCH_BYTES)
 #define FSMF_LASTCHG (FSMF_LASTPROC + MCEIK_MAX_BLOCKS * 4)
-#define FSMF_U0EP (FSMF_LASTCHG + MCEIK_MAX_BLOCKS * 4)
-#define FSMF_ORDER (FSMF_U0EP + MCEIK_MAX_BLOCKS * 2)
+#define FSMF_ORDER (FSMF_LASTCHG + MCEIK_MAX_BLOCKS * 4)
 static inline __host__ __device__ bool fsm_fixed_layout(const FsmLaunch &L, size_t es)
 {
     return es == 4 && L.slow_mode != 0 && L.cell_cache && L.fast_sqrt && L.nrz == 4 && L.ccb <= 64 &&
@@ -98,9 +103,9 @@ static inline __host__ __device__ bool fsm_fixed_layout(const FsmLaunch &L, size
 static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, size_t es, size_t *off)
 {
     if (fsm_fixed_layout(L, es)) {
-        off[11] = FSMF_CINFO; off[9] = FSMF_HALO; off[10] = FSMF_HALO + 128 * 4; off[1] = FSMF_CC;
+        off[11] = FSMF_CINFO; off[9] = FSMF_XR; off[10] = FSMF_XN; off[1] = FSMF_CC;
         off[6] = FSMF_RING; off[7] = FSMF_SCRATCH; off[3] = FSMF_LASTPROC; off[4] = FSMF_LASTCHG;
-        off[5] = FSMF_U0EP; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;          // sf: unused (cells cached)
+        off[5] = FSMF_ORDER; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;          // sf: unused (cells cached)
         off[0] = FSMF_ORDER + mceik_align16((size_t)L.ntiles * 4);
         return off[0] + mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
     }
@@ -112,13 +117,13 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[2] = o; o += mceik_align16(nt * 4);
     off[3] = o; o += mceik_align16(nb * 4);
     off[4] = o; o += mceik_align16(nb * 4);
-    off[5] = o; o += mceik_align16(nb * 2);
+    off[5] = o;
     off[6] = o; o += mceik_align16(nr * 8);
     off[7] = o; o += MCEIK_SCRATCH_BYTES;
     off[8] = o; o += cached ? 0 : 512 * es;
-    off[9] = o; o += 128 * es;
-    off[10] = o; o += 128 * es;
-    off[11] = o; o += nr * 64 * 16;
+    off[9] = o; o += 2 * MCEIK_XROWS * 4 * es;
+    off[10] = o; o += 2 * MCEIK_XROWS * 4 * es;
+    off[11] = o; o += nr * 64 * 8;
     return o;
 }
 static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
@@ -150,7 +155,9 @@ static inline void fsm_geometry(FsmLaunch *L, int es)
     L->nzb = mceik_div_up(L->nz, MCEIK_TILE);
     L->ntiles = L->ntx * L->nty;
     int kb = L->nzb < MCEIK_KB ? L->nzb : MCEIK_KB;
-    while (kb < L->nzb && (long)L->ntiles * mceik_div_up(L->nzb, kb) > MCEIK_MAX_BLOCKS) kb *= 2;
+    // (a z-block index must fit the 7-bit tz field of the column info word)
+    while (kb < L->nzb && ((long)L->ntiles * mceik_div_up(L->nzb, kb) > MCEIK_MAX_BLOCKS || mceik_div_up(L->nzb, kb) > 128))
+        kb *= 2;
     if (kb > L->nzb) kb = L->nzb;
     L->kb = kb;
     L->nzk = mceik_div_up(L->nzb, kb);

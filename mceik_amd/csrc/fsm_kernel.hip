@@ -78,43 +78,13 @@ __device__ __forceinline__ float bload1f(Rsrc r, uint32_t off)
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
-// ---- lane exchange: x neighbours by DPP (lane -+ 1 in a 16-lane row),
-// y neighbours by ds_bpermute (lane -+ 8).  Tile-edge lanes get halo values.
-__device__ __forceinline__ float dpp_from_prev(float v)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float dpp_from_next(float v)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x101, 0xf, 0xf, true));
-}
-__device__ __forceinline__ double dpp_from_prev(double v)
-{
-    unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x111, 0xf, 0xf, false);
-    unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x111, 0xf, 0xf, false);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ double dpp_from_next(double v)
-{
-    unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x101, 0xf, 0xf, false);
-    unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x101, 0xf, 0xf, false);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-// y neighbours: ds_bpermute from lane -/+ 8 (byte addresses precomputed once;
-// lanes 0..7 / 56..63 receive a wrapped value and use the y halo instead)
-__device__ __forceinline__ float bperm(int addr, float v)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
-}
-__device__ __forceinline__ double bperm(int addr, double v)
-{
-    unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    unsigned lo = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)u);
-    unsigned hi = __builtin_amdgcn_ds_bpermute(addr, (int)(unsigned)(u >> 32));
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
+// ---- neighbour exchange through LDS rows.  At the end of every step each
+// lane writes its 8 results (XR row) and its next brick (XN row); the next
+// step reads the x/y-upwind lanes' XR rows (new values of its own z brick)
+// and the downwind lanes' XN rows (old values), tile-edge lanes the halo
+// rows staged in the same arrays.  The row offsets are lane constants, so a
+// node's four x/y neighbours cost no VALU (no DPP moves, no halo selects).
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 // Column order inside a brick: the tile perimeter first -- rows ly = 0 and
 // ly = 7 (slots 0..15), then the x faces lx = 0 and lx = 7 (16..27), then the
@@ -191,13 +161,12 @@ struct Smem {
     float *cc;                   // cell cache [nr][ccb]                   (SLOWMODE 2)
     int *order;                  // diagonal tile order: txs | tys << 16   [ntiles]
     int *lastproc, *lastchg;     // per z-block stream clock of the last visit / last visit with a change
-    unsigned short *u0ep;        // per z-block iteration+1 of the last u0 store
     int *ring;                   // per position (mod nr): block entry tx | ty << 12 | tz << 24, bubble -1;
                                  // then [nr] the z-block ids
     int *scratch;                // debug counters
-    u4v *cinfo;                  // [nr][64] column info of every lane per position
+    u2v *cinfo;                  // [nr][64] column info of every lane per position: {own column, meta}
     R *sf;                       // staged slowness*h (modes 0,1)
-    R *halo;                     // staged halos [32 halo columns][8 z] (halo_col)
+    R *xr;                       // neighbour rows: XR [2 halves][80 rows][4], then XN (same shape)
 };
 
 template <typename R, bool FIXED>
@@ -205,8 +174,8 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
 {
     size_t off[MCEIK_SMEM_ARRAYS];
     if (FIXED) {         // fsm_fixed_layout(): constants (the host checked the predicate)
-        off[11] = FSMF_CINFO; off[9] = FSMF_HALO; off[1] = FSMF_CC; off[6] = FSMF_RING; off[7] = FSMF_SCRATCH;
-        off[3] = FSMF_LASTPROC; off[4] = FSMF_LASTCHG; off[5] = FSMF_U0EP; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;
+        off[11] = FSMF_CINFO; off[9] = FSMF_XR; off[1] = FSMF_CC; off[6] = FSMF_RING; off[7] = FSMF_SCRATCH;
+        off[3] = FSMF_LASTPROC; off[4] = FSMF_LASTCHG; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;
         off[0] = FSMF_ORDER + mceik_align16((size_t)L.ntiles * 4);
     } else {
         fsm_smem_layout(L, sizeof(R), off);
@@ -217,12 +186,11 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     S.order = reinterpret_cast<int *>(base + off[2]);
     S.lastproc = reinterpret_cast<int *>(base + off[3]);
     S.lastchg = reinterpret_cast<int *>(base + off[4]);
-    S.u0ep = reinterpret_cast<unsigned short *>(base + off[5]);
     S.ring = reinterpret_cast<int *>(base + off[6]);
     S.scratch = reinterpret_cast<int *>(base + off[7]);
     S.sf = reinterpret_cast<R *>(base + off[8]);
-    S.halo = reinterpret_cast<R *>(base + off[9]);     // arrays 9 and 10 are contiguous
-    S.cinfo = reinterpret_cast<u4v *>(base + off[11]);
+    S.xr = reinterpret_cast<R *>(base + off[9]);       // arrays 9 (XR) and 10 (XN) are contiguous
+    S.cinfo = reinterpret_cast<u2v *>(base + off[11]);
     return S;
 }
 
@@ -293,10 +261,12 @@ enum {
     C_BC = 16,      // column crosses a boundary-condition box in x and y
     C_BLK = 32,     // the position holds a z-block (not a bubble)
     C_ZH = 64,      // run start inside the column: the z-upwind value comes from HBM
-    F_VALID = 128, F_FIRST = 256, F_LAST = 512, F_SLOW = 1024, F_ZH = 2048
+    C_XOWN = 128,   // x-edge lane whose x neighbour is outside the grid: its x halo is its own column
+    C_YOWN = 256,   // the same for the y halo
+    F_VALID = 128, F_FIRST = 256, F_LAST = 512, F_SLOW = 1024, F_ZH = 2048   // BInfo.fl (meta bits 0-6 +)
 };
-// column info word w: flags (bits 0-6) | tz << 8 | (signed) cell-cache base << 16
-__device__ __forceinline__ int ci_tz(unsigned w) { return (int)((w >> 8) & 0xff); }
+// column info word w: flags (bits 0-8) | tz << 9 (7 bits) | (signed) cell-cache base << 16
+__device__ __forceinline__ int ci_tz(unsigned w) { return (int)((w >> 9) & 0x7f); }
 __device__ __forceinline__ int ci_ccb(unsigned w) { return (int)w >> 16; }
 
 // What a lane needs about one of its bricks.
@@ -325,14 +295,15 @@ __device__ __forceinline__ void block_zcells(const FsmLaunch &L, int kb, int tz,
 }
 
 // Column info of this lane for the tile of a run (entry: tx | ty << 12): the
-// own column and x/y halo offsets, the tile-level flags and the lane's cell
-// column (cyl * ncxt + cxl).  The x/y halo of a tile-edge lane is the
-// neighbour column, or the lane's own column where the grid ends (the
-// reference's missing neighbour is the node itself: the halo then holds
-// exactly the node's old value); interior lanes: OOB.
+// own column offset, the tile-level flags and the lane's cell column
+// (cyl * ncxt + cxl).  The x/y halo of a tile-edge lane is the neighbour
+// column (a lane-constant offset from the own column, halo_delta), or the
+// lane's own column where the grid ends (C_XOWN / C_YOWN: the reference's
+// missing neighbour is the node itself, so the halo then holds exactly the
+// node's old value).
 struct ColTile {
     int tile;                    // tx | ty << 12 of the cached tile, -1 none
-    uint32_t col, hx, hy;
+    uint32_t col;
     int fl, cl;
 };
 template <typename R>
@@ -343,18 +314,15 @@ __device__ __forceinline__ void column_tile(const FsmLaunch &L, const BcBoxes &b
     const int x = tx * 8 + lx, y = ty * 8 + ly;
     const uint32_t st = tile_bytes<R>(L);
     const uint32_t col = (uint32_t)(ty * L.ntx + tx) * st + (uint32_t)colpos(lx, ly) * 128u;
-    uint32_t hx = OOB, hy = OOB;
+    int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
     if (lxs == 0 || lxs == 7) {
         const int xn = x + (((lxs == 0) != (rx != 0)) ? -1 : 1);
-        hx = (xn >= 0 && xn < L.nx) ? (uint32_t)(ty * L.ntx + (xn >> 3)) * st + (uint32_t)colpos(xn & 7, ly) * 128u
-                                     : col;
+        if (!(xn >= 0 && xn < L.nx)) m |= C_XOWN;
     }
     if (lys == 0 || lys == 7) {
         const int yn = y + (((lys == 0) != (ry != 0)) ? -1 : 1);
-        hy = (yn >= 0 && yn < L.ny) ? (uint32_t)((yn >> 3) * L.ntx + tx) * st + (uint32_t)colpos(lx, yn & 7) * 128u
-                                     : col;
+        if (!(yn >= 0 && yn < L.ny)) m |= C_YOWN;
     }
-    int m = (x < L.nx && y < L.ny) ? C_ACT : 0;
     if (tx * 8 + 8 > L.nx || ty * 8 + 8 > L.ny) m |= C_PART;
     if (x == 0 && y == 0) m |= C_00;
     for (int k = 0; k < bc.n; k++) {
@@ -368,7 +336,7 @@ __device__ __forceinline__ void column_tile(const FsmLaunch &L, const BcBoxes &b
     const int cxl = (int)(((unsigned)xc * L.magic_rx) >> 20) - cx0;
     const int cyl = (int)(((unsigned)yc * L.magic_ry) >> 20) - cy0;
     t.tile = entry & 0xffffff;
-    t.col = col; t.hx = hx; t.hy = hy;
+    t.col = col;
     t.fl = m;
     t.cl = cyl * ncxt + cxl;
 }
@@ -381,15 +349,15 @@ __device__ __forceinline__ unsigned column_word(const FsmLaunch &L, int kb, cons
     block_zcells(L, kb, tz, cz0, nczb);
     const int ccb = ri * L.ccb + t.cl * nczb - cz0;
     const int m = t.fl | C_BLK | (u0flag ? C_U0 : 0) | (zh ? C_ZH : 0);
-    return (unsigned)(m | (tz << 8) | (ccb << 16));
+    return (unsigned)(m | (tz << 9) | (ccb << 16));
 }
 
 template <typename R, bool RZ, int ZSH>
 __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Smem<R> &S, const Pos &p, int nstream,
-                                            int lx, int ly, const BcBoxes &bc, const u4v ci)
+                                            int lx, int ly, const BcBoxes &bc, const u2v ci)
 {
     BInfo b;
-    const unsigned meta = ci.w;
+    const unsigned meta = ci.y;
     const int tz = ci_tz(meta);
     const int zb = tz * kb + (RZ ? kb - 1 - p.zbs : p.zbs);
     const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < L.nzb;
@@ -442,15 +410,32 @@ __device__ __forceinline__ int halo_edge_lane(int j)
 {
     return j < 8 ? j * 8 : j < 16 ? (j - 8) * 8 + 7 : j < 24 ? j - 16 : 56 + (j - 24);
 }
-// offset of this lane's half of halo column j at the edge lane's position pe
-template <typename R, bool RZ>
-__device__ __forceinline__ uint32_t halo_offset(const FsmLaunch &L, int kb, const Pos &pe, int nstream, int j,
-                                                int half, const u4v ci)     // ci: the edge lane's column info at pe
+// Byte offset from a tile-edge lane's own column to the neighbour column
+// its halo column j reads (sweep direction rx, ry; he = the edge lane): the
+// neighbour tile (+-1 in x, +-ntx in y) and the column on that tile's facing
+// edge.
+__device__ __forceinline__ uint32_t halo_delta(const FsmLaunch &L, uint32_t tile_bytes, int j, int he, int rx, int ry)
 {
-    const unsigned meta = ci.w;
+    const int lxs = he & 7, lys = he >> 3;
+    const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
+    if (j < 16) {
+        const int dx = ((j < 8) != (rx != 0)) ? -1 : 1;
+        return (uint32_t)(dx * (int)tile_bytes) + (uint32_t)((colpos((lx + dx) & 7, ly) - colpos(lx, ly)) * 128);
+    }
+    const int dy = ((j < 24) != (ry != 0)) ? -1 : 1;
+    return (uint32_t)(dy * L.ntx * (int)tile_bytes) + (uint32_t)((colpos(lx, (ly + dy) & 7) - colpos(lx, ly)) * 128);
+}
+// offset of this lane's half of halo column j at the edge lane's position pe
+// (ci: the edge lane's column info at pe; hbit: C_XOWN for x halos, C_YOWN
+// for y halos; hdelta: halo_delta)
+template <typename R, bool RZ>
+__device__ __forceinline__ uint32_t halo_offset(const FsmLaunch &L, int kb, const Pos &pe, int nstream, int half,
+                                                const u2v ci, unsigned hbit, uint32_t hdelta)
+{
+    const unsigned meta = ci.y;
     const int zb = ci_tz(meta) * kb + (RZ ? kb - 1 - pe.zbs : pe.zbs);
     const bool valid = pos_valid(pe, nstream) && (meta & C_BLK) && zb < L.nzb;
-    const uint32_t base = j < 16 ? ci.y : ci.z;
+    const uint32_t base = ci.x + ((meta & hbit) ? 0u : hdelta);
     return valid ? base + zoff_bytes<R>(zb) + (uint32_t)half * 4u * (uint32_t)sizeof(R) : OOB;
 }
 __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, float (&v)[4])
@@ -464,12 +449,36 @@ __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, double (&v)[4])
     d2v b = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
 }
-template <typename R>
-__device__ __forceinline__ void halo_stage(const Smem<R> &S, int lane, const R (&v)[4])
+// Neighbour rows: XR = S.xr[0 .. 640), XN = S.xr[640 .. 1280), each
+// [half][80 rows][4] (element offsets).  Halo columns go to rows 64..79:
+// j = 0..7 (x-upwind of lanes (0, j)) XR 64 + j, 8..15 (x-downwind of
+// (7, j - 8)) XN 64 + j - 8, 16..23 (y-upwind of (j - 16, 0)) XR 72 + j - 16,
+// 24..31 (y-downwind of (j - 24, 7)) XN 72 + j - 24.
+#define XROW(arr, half, row) ((((arr) * 2 + (half)) * MCEIK_XROWS + (row)) * 4)
+__device__ __forceinline__ int halo_row_off(int lane)
 {
-    R *d = S.halo + lane * 4;            // = [j][half * 4 + i]
+    const int j = lane >> 1, half = lane & 1;
+    return XROW((j >> 3) & 1, half, 64 + ((j >> 4) << 3) + (j & 7));
+}
+template <typename R>
+__device__ __forceinline__ void store4(R *d, const R (&v)[4])
+{
 #pragma unroll
     for (int i = 0; i < 4; i++) d[i] = v[i];
+}
+template <typename R>
+__device__ __forceinline__ void store_row(R *x, int arr, int lane, const R (&v)[8])
+{
+    R *a = x + XROW(arr, 0, lane), *b = x + XROW(arr, 1, lane);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { a[i] = v[i]; b[i] = v[4 + i]; }
+}
+template <typename R>
+__device__ __forceinline__ void load_row(const R *x, int off0, R (&v)[8])   // off0 = XROW(arr, 0, row)
+{
+    const R *a = x + off0, *b = x + off0 + 4 * MCEIK_XROWS;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { v[i] = a[i]; v[4 + i] = b[i]; }
 }
 
 // Loads / stores that most lanes skip (z-upwind nodes of run starts, u0
@@ -738,28 +747,28 @@ __device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R> &S, Stre
 // the grid) and the column segments of all lanes (S.scratch[0], [1]).
 template <typename R>
 __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> &S, const BcBoxes &bc, int entry,
-                                      int zh, int ri, int clock, int it, int lx, int ly, int lxs, int lys, int rx,
+                                      int zh, int ri, int clock, int clock_it, int lx, int ly, int lxs, int lys, int rx,
                                       int ry, ColTile &ct)
 {
-    u4v ci;
+    u2v ci;
     int bid = 0, nbv = 0;
     if (entry >= 0) {
         const int tz = (entry >> 24) & 0xff;
         bid = tz * L.ntiles + (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
         nbv = min(kb, L.nzb - tz * kb);
-        const int u0flag = S.u0ep[bid] != (unsigned short)(it + 1);
+        // first visit of the block in this iteration: no visit since the iteration's first clock
+        const int u0flag = S.lastproc[bid] < clock_it;
         if ((entry & 0xffffff) != ct.tile) column_tile<R>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
-        ci.x = ct.col; ci.y = ct.hx; ci.z = ct.hy;
-        ci.w = column_word(L, kb, ct, tz, ri, u0flag, zh);
+        ci.x = ct.col;
+        ci.y = column_word(L, kb, ct, tz, ri, u0flag, zh);
     } else {
-        ci.x = OOB; ci.y = OOB; ci.z = OOB; ci.w = 0;
+        ci.x = OOB; ci.y = 0;
     }
     const int nact = L.visit_stats && entry >= 0 ? __builtin_popcountll(__ballot(ct.fl & C_ACT)) : 0;
     asm volatile("" ::: "memory");
     S.cinfo[ri * 64 + threadIdx.x] = ci;
     if (threadIdx.x == 0) {
         if (entry >= 0) {
-            S.u0ep[bid] = (unsigned short)(it + 1);
             S.lastproc[bid] = clock;
             if (L.visit_stats) {
                 S.scratch[0] += nbv;
@@ -774,9 +783,10 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> 
 
 // Godunov update without the error code (fast path): fp32 values identical to
 // godunov_bl (a1 == UN or an overflowing / NaN candidate gives UN either way).
-// ff = f*f and ff2 = ff + ff come from the caller (once per slowness cell).
+// ff = f*f, ff2 = ff + ff and ff3 = 3*ff come from the caller (once per
+// slowness cell).
 template <bool FAST>
-__device__ __forceinline__ float godunov_v(float a, float b, float c, float f, float ff, float ff2)
+__device__ __forceinline__ float godunov_v(float a, float b, float c, float f, float ff, float ff2, float ff3)
 {
     // sort by bit pattern (non-negative, non-NaN inputs; see fmin_): v_min3 / v_max3 / v_med3
     const unsigned ia = __builtin_bit_cast(unsigned, a), ib = __builtin_bit_cast(unsigned, b),
@@ -792,11 +802,11 @@ __device__ __forceinline__ float godunov_v(float a, float b, float c, float f, f
     const float d2 = a2 - a1, d3 = a3 - a1;
     const float e = d3 - d2;
     const float d22 = d2 * d2, d33 = d3 * d3;
-    const bool two = (d33 + e * e) >= ff;
+    const float t = d33 + e * e;
+    const bool two = t >= ff;
     const float r2 = ff2 - d22;
     const float sm = d2 + d3;
-    const float q = (d22 + d33) - ff;
-    const float disc = sm * sm - 3.0f * q;
+    const float disc = ff3 - (d22 + t);     // 3D radicand, t shared with the 2D/3D test
     const float rad = two ? r2 : disc;
     const float s = FAST ? sqrt_normal(rad) : __builtin_sqrtf(rad);
     // two: 0.5 * (d2 + s); else (sm + s) * (1/3)  (same products, one multiply)
@@ -807,54 +817,22 @@ __device__ __forceinline__ float godunov_v(float a, float b, float c, float f, f
     return __builtin_bit_cast(float, __builtin_elementwise_min(ix, 0x7f7fffffu));
 }
 template <bool FAST>
-__device__ __forceinline__ double godunov_v(double a, double b, double c, double f, double, double)
+__device__ __forceinline__ double godunov_v(double a, double b, double c, double f, double, double, double)
 {
     int e;
     return godunov(a, b, c, f, e);
 }
 
-// Halo values of a brick (MCEIK_HALO_VEC): the lane's x-halo and y-halo rows
-// (8 z each, only tile-edge lanes use them) read with 16-B LDS loads before
-// the slot loop -- 4 ds_read_b128 per brick instead of 16 ds_read_b32.
-#ifndef MCEIK_HALO_VEC
-#define MCEIK_HALO_VEC 1
-#endif
-// MCEIK_BPERM_EARLY: the brick's 16 y-neighbour ds_bpermutes issued before the
-// slot loop (brick_update) instead of one pair per slot
-#ifndef MCEIK_BPERM_EARLY
-#define MCEIK_BPERM_EARLY 1
-#endif
-__device__ __forceinline__ void lds_row8(const float *p, float (&v)[8])
-{
-    const f4v a = reinterpret_cast<const f4v *>(p)[0], b = reinterpret_cast<const f4v *>(p)[1];
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-__device__ __forceinline__ void lds_row8(const double *p, double (&v)[8])
-{
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const d2v a = reinterpret_cast<const d2v *>(p)[k];
-        v[2 * k] = a.x; v[2 * k + 1] = a.y;
-    }
-}
-
-// x/y neighbour minima and f = s*h of slot pj.  The x and y neighbours come
-// from the other lanes' r (updated in their previous step) and n, which the
-// current step does not modify, so any slot may gather them at any time.
+// x/y neighbour minima and f = s*h of slot pj.  The four neighbour rows
+// (x/y-upwind lanes' new values, downwind lanes' old values, or the halo
+// rows for tile-edge lanes) were read from LDS at the start of the brick.
 template <typename R, int SLOWMODE, int ZSH, bool GENERIC, bool WANTF>
 __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, const R (&c)[8],
-                                          const R (&n)[8], const R (&r)[8], const R (&hx)[8], const R (&hy)[8],
-                                          const R (&ymv)[8], const R (&ypvv)[8], int pj, int aup, int adn, bool xp,
-                                          bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
+                                          const R (&xmr)[8], const R (&xpr)[8], const R (&ymr)[8], const R (&ypr)[8],
+                                          int pj, bool xp, bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
 {
-    const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3;
+    const int lane = threadIdx.x;
     const R self = c[pj];
-    const R xm = dpp_from_prev(r[pj]), xpv = dpp_from_next(n[pj]);
-#if MCEIK_BPERM_EARLY
-    const R ym = ymv[pj], ypv = ypvv[pj];
-#else
-    const R ym = bperm(aup, r[pj]), ypv = bperm(adn, n[pj]);
-#endif
     if (!WANTF) {
     } else if (SLOWMODE == 2) {
         if (ZSH >= 0 && !GENERIC) {
@@ -868,19 +846,7 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
     } else {
         fv = S.sf[pj * 64 + lane];
     }
-#if MCEIK_HALO_VEC
-    const R hxv = hx[pj], hyv = hy[pj];
-#else
-    R hxv = S.halo[((lxs == 7 ? 8 : 0) + lys) * 8 + pj];
-    R hyv = S.halo[((lys == 7 ? 24 : 16) + lxs) * 8 + pj];
-    // keep the LDS reads unconditional (hipcc otherwise sinks them into
-    // a branch for the few edge lanes, with an lgkmcnt(0) wait inside)
-    asm volatile("" : "+v"(hxv), "+v"(hyv));
-#endif
-    R xup = lxs > 0 ? xm : hxv;
-    R xdn = lxs < 7 ? xpv : hxv;
-    R yup = lys > 0 ? ym : hyv;
-    R ydn = lys < 7 ? ypv : hyv;
+    R xup = xmr[pj], xdn = xpr[pj], yup = ymr[pj], ydn = ypr[pj];
     if (GENERIC) {
         xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
     }
@@ -913,28 +879,19 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
     // z-upwind value of slot 0: the previous brick of the lane's sequence, or
     // (run start inside the column) the node loaded from HBM
     const R zprev = (fl & F_ZH) ? zc : r[RZ ? 0 : 7];
-    int aup = ((lane - 8) & 63) * 4, adn = ((lane + 8) & 63) * 4;
-    asm volatile("" : "+v"(aup), "+v"(adn));
-    R hx[8], hy[8], ymv[8], ypvv[8];
-    if (MCEIK_HALO_VEC) {
+    // the four neighbour rows (sweep-relative lanes: -1 / -8 upwind in XR,
+    // +1 / +8 downwind in XN; tile-edge lanes read the halo rows)
+    R xmr[8], xpr[8], ymr[8], ypr[8];
+    {
         const int lxs = lane & 7, lys = lane >> 3;
-        lds_row8(S.halo + ((lxs == 7 ? 8 : 0) + lys) * 8, hx);
-        lds_row8(S.halo + ((lys == 7 ? 24 : 16) + lxs) * 8, hy);
+        load_row(S.xr, XROW(0, 0, lxs > 0 ? lane - 1 : 64 + lys), xmr);
+        load_row(S.xr, XROW(0, 0, lys > 0 ? lane - 8 : 72 + lxs), ymr);
+        load_row(S.xr, XROW(1, 0, lxs < 7 ? lane + 1 : 64 + lys), xpr);
+        load_row(S.xr, XROW(1, 0, lys < 7 ? lane + 8 : 72 + lxs), ypr);
     }
-    if (MCEIK_BPERM_EARLY) {
-        // all y-neighbour exchanges of the brick up front (r holds the previous
-        // step's values until slot j overwrites r[pj], n is not written): the
-        // LDS latency then overlaps the z chain instead of stalling each slot
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            ymv[i] = bperm(aup, r[i]);
-            ypvv[i] = bperm(adn, n[i]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // fast fp32 path over the LDS cell cache: f, f*f, 2f*f per cell
+    // fast fp32 path over the LDS cell cache: f, f*f, 2f*f, 3f*f per cell
     constexpr bool CELLF = SLOWMODE == 2 && ZSH >= 0 && !GENERIC && sizeof(R) == 4;
-    R fc = 0, ffc = 0, ff2c = 0;
+    R fc = 0, ffc = 0, ff2c = 0, ff3c = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const int pj = RZ ? 7 - j : j;
@@ -942,14 +899,14 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
         const int pnext = RZ ? pj - 1 : pj + 1;
         const R self = c[pj];
         R ux, uy, fv;
-        gather_xy<R, SLOWMODE, ZSH, GENERIC, !CELLF>(L, S, b0, c, n, r, hx, hy, ymv, ypvv, pj, aup, adn, xp, xn, yp,
-                                                     yn, ux, uy, fv);
+        gather_xy<R, SLOWMODE, ZSH, GENERIC, !CELLF>(L, S, b0, c, xmr, xpr, ymr, ypr, pj, xp, xn, yp, yn, ux, uy, fv);
         if (CELLF) {
             // one LDS read and one f*f per slowness cell (2^ZSH slots)
             if (j == 0 || (pj >> (ZSH < 0 ? 0 : ZSH)) != (pprev >> (ZSH < 0 ? 0 : ZSH))) {
                 fc = (R)S.cc[b0.ccb + (pj >> (ZSH < 0 ? 0 : ZSH))];
                 ffc = fc * fc;
                 ff2c = ffc + ffc;
+                ff3c = (R)3 * ffc;
             }
             fv = fc;
         }
@@ -975,7 +932,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
             if ((fl & C_00) && zabs == 0) ierr_last = upd ? e : 0;
         } else {
             const R ffv = CELLF ? ffc : fv * fv;
-            nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv, ffv, CELLF ? ff2c : ffv + ffv));
+            nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv, ffv, CELLF ? ff2c : ffv + ffv, CELLF ? ff3c : (R)3 * ffv));
         }
         const bool dec = nv < self;
         nc |= dec && self >= T;
@@ -992,7 +949,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
 // nchg: per-lane count of changed column segments (visit statistics).
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
-                                     const Smem<R> &S, int rx, int ry, int it, int clock0,
+                                     const Smem<R> &S, int rx, int ry, int clock_it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned &nchg)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
@@ -1004,6 +961,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 
     // halo loader role of this lane (halo_edge_lane)
     const int hj = lane >> 1, hh = lane & 1, he = halo_edge_lane(hj), hd = (he & 7) + (he >> 3);
+    const unsigned hbit = hj < 16 ? C_XOWN : C_YOWN;
+    const uint32_t hdelta = halo_delta(L, tile_bytes<R>(L), hj, he, rx, ry);
+    const int hso = halo_row_off(lane);
 
     // stream bookkeeping (wave-uniform)
     Stream st;
@@ -1029,7 +989,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             nstream = pos;
             break;
         }
-        admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
+        admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, clock_it, lx, ly, lxs, lys, rx, ry, ct);
         if (SLOWMODE == 2 && e >= 0) {
             cc_issue<CCR>(L, kb, sr, e, ccv, ccsize);
             TRAFU(S, 5, ccsize * 4);
@@ -1051,7 +1011,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     Pos pe;                              // the halo's edge lane position (vb+2 in the loop)
     pos_init(pe, -hd, kb, nr);
     {
-        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]);
+        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, S.cinfo[pe.ri * 64 + he], hbit, hdelta);
         bload4(ur, ho, hq);
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
@@ -1063,7 +1023,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     bload8(ur, b1.seg, n);
     pos_adv(pe, kb, nr);
     {
-        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, S.cinfo[pe.ri * 64 + he]);
+        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, S.cinfo[pe.ri * 64 + he], hbit, hdelta);
         bload4(ur, ho, hn);   // halos of vb+1
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
@@ -1082,7 +1042,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         r[i] = UN;
         if (SLOWMODE != 2) S.sf[i * 64 + lane] = fq[i] * hr;
     }
-    halo_stage<R>(S, lane, hq);
+    store4(S.xr + hso, hq);                       // halos of vb0
+    store_row(S.xr, 0, lane, r);                   // no results yet (u_nan)
+    store_row(S.xr, 1, lane, n);                   // brick vb0 + 1
 #pragma unroll
     for (int i = 0; i < 4; i++) hq[i] = hn[i];
     // Wait for the prologue's loads here, once per sweep: a register the loop
@@ -1135,7 +1097,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             if (e == -2) {
                 nstream = pos;
             } else {
-                admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, it, lx, ly, lxs, lys, rx, ry, ct);
+                admit<R>(L, kb, S, bc, e, zh, dri, clock0 + pos, clock_it, lx, ly, lxs, lys, rx, ry, ct);
                 if (SLOWMODE == 2 && e >= 0) {
                     cc_issue<CCR>(L, kb, sr, e, ccv, ccsize);
                     TRAFU(S, 5, ccsize * 4);
@@ -1162,7 +1124,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         // latency per step instead of two)
         pos_adv(p3, kb, nr);
         pos_adv(pe, kb, nr);
-        const u4v ci3 = S.cinfo[p3.ri * 64 + lane], cie = S.cinfo[pe.ri * 64 + he];
+        const u2v ci3 = S.cinfo[p3.ri * 64 + lane], cie = S.cinfo[pe.ri * 64 + he];
         __builtin_amdgcn_sched_barrier(0);     // keep the two reads ahead of every use
         const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, ci3);
         if (AH == 3) {
@@ -1176,7 +1138,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
         }
         {
-            const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hj, hh, cie);
+            const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, cie, hbit, hdelta);
             bload4(ur, ho, hn);
             TRAF(S, 1, ho != OOB, 4 * sizeof(R));
             TRAF(S, 0, b3.seg != OOB, 8 * sizeof(R));
@@ -1218,7 +1180,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #pragma unroll
             for (int i = 0; i < 8; i++) S.sf[i * 64 + lane] = fq[i] * hr;
         }
-        halo_stage<R>(S, lane, hq);
+        store4(S.xr + hso, hq);
         R nn[8];
         if (PAIR) {
             pair_finish(qa, qb, reinterpret_cast<float (&)[8]>(nn));
@@ -1229,6 +1191,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (AH == 3) q[i] = p[i];
             }
         }
+        // neighbour rows for the next step: this step's results, the next brick
+        store_row(S.xr, 0, lane, r);
+        store_row(S.xr, 1, lane, nn);
         if (!ROT) {
 #pragma unroll
             for (int i = 0; i < 4; i++) hq[i] = hn[i];
@@ -1487,7 +1452,6 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         // initial visit counts as in flight.
         for (int t = lane; t < L.nblocks; t += 64) {
             S.lastproc[t] = -2; S.lastchg[t] = -3;
-            S.u0ep[t] = 0;
         }
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
 #ifdef MCEIK_TRAFFIC
@@ -1523,10 +1487,10 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
                         clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last, nchg);
+                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg);
                     else
                         clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, it, clock, notconv, ierr_last, nchg);
+                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg);
 #ifdef MCEIK_STEPSTATS
                     {   // experiment: visited blocks of this sweep that did not change
                         const int c1 = clock - L.infl;

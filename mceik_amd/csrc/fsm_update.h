@@ -57,7 +57,7 @@ __device__ __forceinline__ double godunov(double a, double b, double c, double f
 // denormal rescale and zero/inf fix-up).  Used only where the radicand that
 // is finally selected is provably a normal float: on the MCMC path f = h*s >=
 // h/vmax (checked on the host) and the selected radicand exceeds f^2 (2D:
-// 2f^2 - d2^2 with d2 < f; 3D: 3f^2 - d2^2 - (d3^2 + (d3-d2)^2) with both
+// 2f^2 - d2^2 with d2 < f; 3D: 3f^2 - (d2^2 + (d3^2 + (d3-d2)^2)) with both
 // terms < f^2).
 __device__ __forceinline__ float sqrt_normal(float x)
 {
@@ -84,11 +84,11 @@ __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, 
     const float d2 = a2 - a1, d3 = a3 - a1;
     const float ff = f * f, e = d3 - d2;
     const float d22 = d2 * d2, d33 = d3 * d3;
-    const bool two = (d33 + e * e) >= ff;
+    const float t = d33 + e * e;
+    const bool two = t >= ff;
     const float r2 = (ff + ff) - d22;
     const float sm = d2 + d3;
-    const float q = (d22 + d33) - ff;
-    const float disc = sm * sm - 3.0f * q;
+    const float disc = (3.0f * ff) - (d22 + t);      // 3f^2 - (d2^2 + d3^2 + (d3-d2)^2)
     const float rad = two ? r2 : disc;
     const float s = FAST ? sqrt_normal(rad) : __builtin_sqrtf(rad);
     const float y23 = two ? 0.5f * (d2 + s) : (sm + s) * (1.0f / 3.0f);
