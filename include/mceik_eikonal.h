@@ -140,6 +140,9 @@ typedef struct mceik_fsm_batch {
                                    loads, halo loads, z-upwind loads, own stores, u0 stores, cell loads,
                                    convergence-check loads, init fill + table gather); counted only by
                                    an accounting build (-DMCEIK_TRAFFIC), else untouched; or NULL */
+    int step_z;                 /* z nodes per macro step of the sweep kernel: 0 = the launch's choice
+                                   (16 for the fp32 cell-cache instance, else 8), 8 = force the 8-z
+                                   kernel (A/B measurements, parity tests); results are identical */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */
@@ -148,6 +151,9 @@ size_t mceik_fsm_workspace_bytes(const mceik_fsm_batch *b);
  * synchronisation and no allocation: capturable in a hipGraph. 0 = ok. */
 int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes,
                           void *stream);
+
+/* z nodes per macro step the launch of this batch runs (8 or 16; diagnostic). */
+int mceik_fsm_step_z(const mceik_fsm_batch *b);
 
 /* Algorithmic HBM bytes of one node visit in one sweep (roofline accounting). */
 double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b);

@@ -24,7 +24,7 @@ class FsmBatch(C.Structure):
                 ("u_out", C.c_void_p), ("niter", C.c_void_p), ("ierr", C.c_void_p),
                 ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
                 ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p),
-                ("max_waves", C.c_int), ("traffic", C.c_void_p)]
+                ("max_waves", C.c_int), ("traffic", C.c_void_p), ("step_z", C.c_int)]
 
 
 class RelocateBatch(C.Structure):
@@ -81,7 +81,8 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_i
            "eikonal3d_finalize", "locate3d_gridsearch__double64", "locate3d_gridsearch__float64",
            "locate_l2_gridSearch__double64",
            "locate_l2_gridSearch__float64", "mceik_relocate",
-           "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_memcpy",
+           "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_fsm_step_z",
+           "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
            "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize")
@@ -115,6 +116,8 @@ def lib():
     L.locate_l2_gridSearch__double64.argtypes = [C.c_int] * 4 + [C.c_double] + [C.c_void_p] * 7
     L.mceik_fsm_workspace_bytes.restype = C.c_size_t
     L.mceik_fsm_workspace_bytes.argtypes = [C.POINTER(FsmBatch)]
+    L.mceik_fsm_step_z.restype = C.c_int
+    L.mceik_fsm_step_z.argtypes = [C.POINTER(FsmBatch)]
     L.mceik_fsm_bytes_per_node_sweep.restype = C.c_double
     L.mceik_fsm_bytes_per_node_sweep.argtypes = [C.POINTER(FsmBatch)]
     L.mceik_fsm_batch_solve.restype = C.c_int

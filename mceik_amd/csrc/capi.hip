@@ -21,6 +21,8 @@
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st);
 int fsm_occupancy(const FsmLaunch &L, int is_double);
+size_t fsm_launch_lds_bytes(const FsmLaunch &L, int is_double);
+int fsm_launch_kind(const FsmLaunch &L, int is_double);
 hipError_t fsm_to_brick_f64(const double *src, void *dst, int dst_double, const FsmLaunch &L, int nfield, hipStream_t st);
 hipError_t fsm_from_brick_f64(const void *src, int src_double, double *dst, const FsmLaunch &L, int nfield, hipStream_t st);
 hipError_t fsm_from_brick_f32(const float *src, float *dst, const FsmLaunch &L, int nfield, hipStream_t st);
@@ -115,6 +117,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.solve_clock = b->solve_clock;
     L.max_waves = b->max_waves;
     L.traffic = b->traffic;
+    L.step_z = b->step_z;
 }
 
 static int g_device_cus = 0;
@@ -164,8 +167,8 @@ static int batch_waves(const FsmLaunch &L, int is_double)
     if (w > L.nsolve) w = L.nsolve;
     static const bool report = getenv("MCEIK_LAUNCH_REPORT") != nullptr;
     if (report)
-        fprintf(stderr, "mceik fsm launch: %d waves/CU (occupancy), %ld resident waves, %zu B LDS per wave\n", per_cu,
-                w, fsm_lds_bytes(L, is_double ? 8 : 4));
+        fprintf(stderr, "mceik fsm launch: %d-z steps, %d waves/CU (occupancy), %ld resident waves, %zu B LDS per wave\n",
+                fsm_launch_kind(L, is_double), per_cu, w, fsm_launch_lds_bytes(L, is_double));
     return (int)(w < 1 ? 1 : w);
 }
 
@@ -207,6 +210,14 @@ extern "C" size_t mceik_fsm_workspace_bytes(const mceik_fsm_batch *b)
     return ws_layout(b).total;
 }
 
+extern "C" int mceik_fsm_step_z(const mceik_fsm_batch *b)
+{
+    if (!b) return 0;
+    FsmLaunch L;
+    fill_launch(L, b);
+    return fsm_launch_kind(L, b->precision == 64);
+}
+
 extern "C" double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b)
 {
     // u read + u write per node visit; slowness read once per node per model
@@ -234,7 +245,7 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
             fprintf(stderr, "mceik_fsm_batch_solve: one travel-time field must stay below 2 GiB\n");
             return 1;
         }
-        if (fsm_lds_bytes(G, b->precision == 64 ? 8 : 4) > MCEIK_MAX_LDS) {
+        if (fsm_launch_lds_bytes(G, b->precision == 64) > MCEIK_MAX_LDS) {
             fprintf(stderr, "mceik_fsm_batch_solve: %d x %d x %d z-blocks exceed the LDS block tables\n", G.ntx, G.nty,
                     G.nzk);
             return 1;

@@ -1,0 +1,883 @@
+// fsm16_kernel.hip -- the fp32 cell-cache sampler instance of the batched
+// fast-sweeping solve with 16-z macro steps (gfx950).
+//
+// Same schedule and update DAG as fsm_kernel.hip (EIKONAL3D_FSM /
+// EVAL_UPDATE3D / UPDATE3D / SOLVE_HAMILTONIAN3D, fsm3d.f90:28-99, 419-693;
+// DESIGN.md s.3): one 64-lane wave per (model, station) solve, an 8x8 column
+// tile per stream position, lane (lx, ly) one step behind its upwind x/y
+// neighbours, z-blocks admitted only when their inputs changed.  What differs
+// is the step: a lane updates 16 z per step, half of its column's 128-B line
+// (32 fp32 z), so every line is read in two 64-B pieces one step apart instead
+// of four 32-B pieces over four steps.  With ~100 lines open per wave and 256
+// waves per XCD sharing a 4 MB L2, the 8-z kernel re-fetched lines between
+// pieces (1.7x the requested read bytes) and wrote every changed 32-B segment
+// as a 64-B request (2x); the 16-z step halves both the re-fetch chances and
+// the write granularity loss, and the per-step bookkeeping is spread over
+// twice the nodes.  Results are bitwise those of the 8-z kernel and the fp32
+// twin (oracle/fsm_impl.inc): the node update order is a topological order of
+// the same DAG and every skipped block is provably unchanged.
+//
+// Instance: fp32, inversion-cell slowness through the LDS cell cache
+// (f = s*h per cell), nrz = 4 (a brick's 16 slots cover 4 cells in z), the
+// correctly rounded fast sqrt (host-validated), L.kb even and >= 4.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "fsm_common.h"
+#include "fsm_device.h"
+#include "fsm_update.h"
+
+namespace {
+
+// byte offset of 16-z brick zb inside a column's line group (two per line)
+__device__ __forceinline__ uint32_t zoff16(int zb)
+{
+    const uint32_t u = (uint32_t)zb;
+    return ((u >> 1) << 13) | ((u & 1u) << 6);
+}
+
+// ---- LDS ------------------------------------------------------------------
+struct Smem16 {
+    int *box;                    // BC boxes [nsrc][6]
+    float *cc;                   // cell cache [nr][ccb] (f = s*h)
+    int *order;                  // diagonal tile order: txs | tys << 16
+    unsigned short *lastproc;    // per z-block clock (relative to the iteration) of the last visit
+    unsigned short *lastchg;     //   ... of the last visit that changed it
+    int *ring_e, *ring_b;        // per position (mod nr): entry tx | ty << 12 | tz << 24 (bubble -1), block id
+    unsigned *ring_base;         //   ... byte offset of the tile's line groups
+    int *scratch;                // visit statistics / traffic counters
+    float *xr;                   // neighbour rows XR [4][80][4], then XN (same shape)
+    unsigned *meta;              // [nr][64] column meta (flags | tz << 9 | cell-cache base << 16)
+};
+template <bool FIXED>
+__device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char *base)
+{
+    size_t off[MCEIK_SMEM16_ARRAYS];
+    if (FIXED) {         // fsm16_fixed_layout(): constants (checked on the host)
+        off[8] = F16_CINFO; off[7] = F16_XR; off[1] = F16_CC; off[5] = F16_RING; off[6] = F16_SCRATCH;
+        off[3] = F16_LASTPROC; off[4] = F16_LASTCHG; off[2] = F16_ORDER;
+        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 4);
+    } else {
+        fsm16_smem_layout(L, off);
+    }
+    const int nr = fsm16_geo(L).nr;
+    Smem16 S;
+    S.box = reinterpret_cast<int *>(base + off[0]);
+    S.cc = reinterpret_cast<float *>(base + off[1]);
+    S.order = reinterpret_cast<int *>(base + off[2]);
+    S.lastproc = reinterpret_cast<unsigned short *>(base + off[3]);
+    S.lastchg = reinterpret_cast<unsigned short *>(base + off[4]);
+    S.ring_e = reinterpret_cast<int *>(base + off[5]);
+    S.ring_b = S.ring_e + (FIXED ? F16_NR : nr);
+    S.ring_base = reinterpret_cast<unsigned *>(S.ring_b + (FIXED ? F16_NR : nr));
+    S.scratch = reinterpret_cast<int *>(base + off[6]);
+    S.xr = reinterpret_cast<float *>(base + off[7]);
+    S.meta = reinterpret_cast<unsigned *>(base + off[8]);
+    return S;
+}
+
+// Neighbour rows (element offsets into S.xr): array arr (0 = XR: a lane's
+// results of its last step; 1 = XN: its next brick), quarter q (4 z), row
+// (lane 0..63, halo rows 64..79 as in fsm_kernel.hip).
+#define XROW16(arr, q, row) (((((arr) * 4 + (q)) * MCEIK_XROWS) + (row)) * 4)
+typedef float f4v16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_w4(float *p, float a, float b, float c, float d)
+{
+    *reinterpret_cast<f4v16 *>(p) = f4v16{a, b, c, d};
+}
+__device__ __forceinline__ void lds_r4(const float *p, float &a, float &b, float &c, float &d)
+{
+    const f4v16 v = *reinterpret_cast<const f4v16 *>(p);
+    a = v.x; b = v.y; c = v.z; d = v.w;
+}
+__device__ __forceinline__ void store_row16(float *x, int arr, int lane, const float (&v)[16])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) lds_w4(x + XROW16(arr, q, lane), v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+__device__ __forceinline__ void load_row16(const float *x, int arr, int row, float (&v)[16])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) lds_r4(x + XROW16(arr, q, row), v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+// half h (8 z: quarters 2h, 2h+1) of a row
+__device__ __forceinline__ void load_half16(const float *x, int arr, int row, int h, float (&v)[8])
+{
+    lds_r4(x + XROW16(arr, 2 * h, row), v[0], v[1], v[2], v[3]);
+    lds_r4(x + XROW16(arr, 2 * h + 1, row), v[4], v[5], v[6], v[7]);
+}
+// halo staging: lane k holds half (k & 1) of halo column j = k >> 1
+__device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v)[8])
+{
+    const int j = lane >> 1, h = lane & 1;
+    const int arr = (j >> 3) & 1, row = 64 + ((j >> 4) << 3) + (j & 7);
+    lds_w4(x + XROW16(arr, 2 * h, row), v[0], v[1], v[2], v[3]);
+    lds_w4(x + XROW16(arr, 2 * h + 1, row), v[4], v[5], v[6], v[7]);
+}
+
+// ---- global loads / stores of 64-B segments ------------------------------
+// Pair-coalesced (lanes 2i, 2i+1 = x neighbours): each instruction makes both
+// lanes of a pair read the same line, so it touches 32 lines instead of 64.
+//   i0: even own q0,     odd partner's q1     (even's line)
+//   i1: even own q2,     odd partner's q3     (even's line)
+//   i2: even partner q0, odd own q1           (odd's line)
+//   i3: even partner q2, odd own q3           (odd's line)
+// even then holds E0 E2 O0 O2 and odd E1 E3 O1 O3; seg_finish swaps the
+// partner's quarters (DPP quad_perm [1,0,3,2]).
+__device__ __forceinline__ void seg_issue(Rsrc r, uint32_t seg, float (&a)[16])
+{
+    const bool odd = threadIdx.x & 1;
+    const uint32_t segp = dpp_swap_pair(seg);
+    float t[4];
+    bload4(r, odd ? segp + 16u : seg, t);
+    a[0] = t[0]; a[1] = t[1]; a[2] = t[2]; a[3] = t[3];
+    bload4(r, odd ? segp + 48u : seg + 32u, t);
+    a[4] = t[0]; a[5] = t[1]; a[6] = t[2]; a[7] = t[3];
+    bload4(r, odd ? seg + 16u : segp, t);
+    a[8] = t[0]; a[9] = t[1]; a[10] = t[2]; a[11] = t[3];
+    bload4(r, odd ? seg + 48u : segp + 32u, t);
+    a[12] = t[0]; a[13] = t[1]; a[14] = t[2]; a[15] = t[3];
+}
+__device__ __forceinline__ void seg_finish(const float (&a)[16], float (&v)[16])
+{
+    const bool odd = threadIdx.x & 1;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        // even sends its O0 O2 (a[8..15]), odd its E1 E3 (a[0..7])
+        const float send = odd ? a[i] : a[8 + i];
+        const float recv = __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(unsigned, send)));
+        const int q = i >> 2, k = i & 3;       // q = 0: quarter 0/1 pair, q = 1: quarter 2/3 pair
+        // even: own quarters 0 and 2 = a[4q + k] (i0, i1), received 1 and 3
+        // odd:  own quarters 1 and 3 = a[8 + 4q + k] (i2, i3), received 0 and 2
+        v[8 * q + k] = odd ? recv : a[4 * q + k];
+        v[8 * q + 4 + k] = odd ? a[8 + 4 * q + k] : recv;
+    }
+}
+// changed segments only: the same pairing for the write-back
+__device__ __forceinline__ void seg_store(Rsrc r, uint32_t seg, bool chg, const float (&v)[16])
+{
+    const bool odd = threadIdx.x & 1;
+    const uint32_t own = chg ? seg : OOB;
+    const uint32_t oth = dpp_swap_pair(own);
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        // even sends its quarters 1, 3; odd its quarters 0, 2
+        const int q = i >> 2, k = i & 3;
+        const float send = odd ? v[8 * q + k] : v[8 * q + 4 + k];
+        x[i] = __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(unsigned, send)));
+    }
+    // i0: even own q0 | odd partner's q1 (x = even's q1)      i1: even own q2 | odd partner's q3
+    // i2: even partner's q0 (x = odd's q0) | odd own q1        i3: even partner's q2 | odd own q3
+    bstore4(r, odd ? oth + 16u : own, odd ? x[0] : v[0], odd ? x[1] : v[1], odd ? x[2] : v[2], odd ? x[3] : v[3]);
+    bstore4(r, odd ? oth + 48u : own + 32u, odd ? x[4] : v[8], odd ? x[5] : v[9], odd ? x[6] : v[10],
+            odd ? x[7] : v[11]);
+    bstore4(r, odd ? own + 16u : oth, odd ? v[4] : x[0], odd ? v[5] : x[1], odd ? v[6] : x[2], odd ? v[7] : x[3]);
+    bstore4(r, odd ? own + 48u : oth + 32u, odd ? v[12] : x[4], odd ? v[13] : x[5], odd ? v[14] : x[6],
+            odd ? v[15] : x[7]);
+}
+__device__ __forceinline__ void store16_plain(Rsrc r, uint32_t off, const float (&v)[16])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) bstore4(r, off + 16u * q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+// ---- brick / halo addressing ------------------------------------------------
+struct BInfo16 {
+    uint32_t seg;            // own 64-B segment (OOB if none)
+    uint32_t zh;             // z-upwind node of a run start (prefetch only)
+    int zb, fl, ccb, ri, bid, clk, bcm;
+};
+template <bool RZ>
+__device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, const Pos &p,
+                                                int nstream, int lx, int ly, const BcBoxes &bc, unsigned meta,
+                                                uint32_t col)
+{
+    BInfo16 b;
+    const int tz = ci_tz(meta);
+    const int zb = tz * g.kb + (RZ ? g.kb - 1 - p.zbs : p.zbs);
+    const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < g.nzb;
+    b.seg = valid ? col + zoff16(zb) : OOB;
+    const int zu = RZ ? zb * 16 + 16 : zb * 16 - 1;          // z-upwind node of the brick's first slot
+    b.zh = (valid && (meta & C_ZH) && p.zbs == 0) ? col + zoff16(zu >> 4) + (uint32_t)(zu & 15) * 4u : OOB;
+    b.zb = valid ? zb : 0;
+    b.ri = p.ri;
+    b.clk = p.sp;
+    b.bid = S.ring_b[p.ri];
+    int fl = valid ? (int)((meta & 0x7f) | F_VALID) : 0;
+    if (zb == (RZ ? g.nzb - 1 : 0)) fl |= F_FIRST;
+    if (zb == (RZ ? 0 : g.nzb - 1)) fl |= F_LAST;
+    if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
+    bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && zb * 16 + 16 > L.nz);
+    b.bcm = 0;
+    if (__any(fl & C_BC)) {
+        // BC z-slots of this column segment (rare: columns through a source box)
+        const int e = S.ring_e[p.ri];
+        const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
+        unsigned m = 0;
+        if (fl & C_BC) {
+            for (int k = 0; k < bc.n; k++) {
+                const int *q = bc.box + 6 * k;
+                if (x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]) {
+                    int lo = q[4] - zb * 16, hi = q[5] - zb * 16;
+                    lo = lo < 0 ? 0 : lo; hi = hi > 15 ? 15 : hi;
+                    if (lo <= hi) m |= ((2u << hi) - (1u << lo));
+                }
+            }
+        }
+        b.bcm = (int)m;
+        slow |= m != 0;
+    }
+    if (slow) fl |= F_SLOW;
+    b.fl = fl;
+    b.ccb = ci_ccb(meta) + zb * 4;                             // nrz = 4: cell of node z = base + z / 4
+    return b;
+}
+// this lane's half (8 z) of halo column j at the edge lane's position pe
+template <bool RZ>
+__device__ __forceinline__ uint32_t halo_offset16(const Fsm16Geo &g, const Pos &pe, int nstream, int half,
+                                                  unsigned meta, uint32_t col, unsigned hbit, uint32_t hdelta)
+{
+    const int zb = ci_tz(meta) * g.kb + (RZ ? g.kb - 1 - pe.zbs : pe.zbs);
+    const bool valid = pos_valid(pe, nstream) && (meta & C_BLK) && zb < g.nzb;
+    const uint32_t base = col + ((meta & hbit) ? 0u : hdelta);
+    return valid ? base + zoff16(zb) + (uint32_t)half * 32u : OOB;
+}
+
+// ---- stream decisions (as decide() in fsm_kernel.hip, 16-bit clocks) -----
+template <bool RZ>
+__device__ __forceinline__ int decide16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, Stream &st, int C,
+                                        int rx, int ry, int &zh)
+{
+    const int lane = threadIdx.x;
+    const int nt = L.ntiles, nzk = L.nzk;
+    zh = 0;
+    if (st.tile < 0) {
+        while (st.cursor < nt) {
+            const int k = st.cursor + lane;
+            int k0 = nzk, entry = 0;
+            if (k < nt) {
+                const int o = S.order[k];
+                const int txs = o & 0xffff, tys = o >> 16;
+                const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+                const int id = ty * L.ntx + tx;
+                const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
+                const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -1;
+                entry = tx | (ty << 12);
+                for (int kz = 0; kz < nzk; kz++) {
+                    const int tz = RZ ? nzk - 1 - kz : kz;
+                    const int b = tz * nt + id;
+                    const int lp = S.lastproc[b];
+                    bool d = S.lastchg[b] >= lp;
+                    if (tx > 0) d |= S.lastchg[b - 1] > lp;
+                    if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
+                    if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
+                    if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
+                    if (tz > 0) d |= S.lastchg[b - nt] > lp;
+                    if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
+                    if (xu >= 0) d |= (int)S.lastproc[tz * nt + xu] > C - g.infl;
+                    if (yu >= 0) d |= (int)S.lastproc[tz * nt + yu] > C - g.infl;
+                    if (d) { k0 = kz; break; }
+                }
+            }
+            const unsigned long long m = __ballot(k0 < nzk);
+            if (m) {
+                const int first = __builtin_ctzll(m);
+                st.cursor += first + 1;
+                st.tile = __builtin_amdgcn_readfirstlane(__shfl(entry, first, 64));
+                st.k0 = st.k = __builtin_amdgcn_readfirstlane(__shfl(k0, first, 64));
+                break;
+            }
+            st.cursor += 64;
+        }
+        if (st.tile < 0) return -2;
+        // bubbles before the run: block k sits at position pos + wait + (k - k0),
+        // which must be >= vis positions after its upwind x/y neighbours' visits
+        const int tx = st.tile & 0xfff, ty = st.tile >> 12;
+        const int txs = rx ? L.ntx - 1 - tx : tx, tys = ry ? L.nty - 1 - ty : ty;
+        const int id = ty * L.ntx + tx;
+        int need = 0;
+        for (int kz = st.k0 + lane; kz < nzk; kz += 64) {
+            const int tz = RZ ? nzk - 1 - kz : kz;
+            int p = -0x40000000;
+            if (txs > 0) p = max(p, (int)S.lastproc[tz * nt + id + (rx ? 1 : -1)]);
+            if (tys > 0) p = max(p, (int)S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)]);
+            need = max(need, p + g.vis - (kz - st.k0) - C);
+        }
+        st.wait = __builtin_amdgcn_readfirstlane(wave_max(need));
+    }
+    if (st.wait > 0) {
+        st.wait--;
+        return -1;
+    }
+    const int kz = st.k;
+    zh = kz == st.k0 && kz > 0;
+    const int tz = RZ ? nzk - 1 - kz : kz;
+    const int e = st.tile | (tz << 24);
+    if (++st.k == nzk) st.tile = -1;
+    return e;
+}
+
+// Admit position (ring slot ri, relative clock C): every lane writes its
+// column meta, lane 0 the ring entry, block id, tile base and the block's
+// visit clock.  u0 flag: the block's first visit in this iteration
+// (lastproc is rebased to 1 at every iteration start, iter_norm()).
+__device__ __forceinline__ void admit16(const FsmLaunch &L, const Smem16 &S, const BcBoxes &bc, int entry, int zh,
+                                        int ri, int C, int lx, int ly, int lxs, int lys, int rx, int ry, ColTile &ct)
+{
+    unsigned meta = 0;
+    int bid = 0, nbv = 0;
+    uint32_t base = 0;
+    if (entry >= 0) {
+        const int tz = (entry >> 24) & 0xff, tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
+        bid = tz * L.ntiles + tx + ty * L.ntx;
+        nbv = min(L.kb, L.nzb - tz * L.kb);          // 8-z bricks of the block (visit statistics)
+        const int u0flag = S.lastproc[bid] < 64;       // no visit since the iteration started (clock 64)
+        if ((entry & 0xffffff) != ct.tile) column_tile<float>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
+        meta = column_word(L, L.kb, ct, tz, ri, u0flag, zh);
+        base = (uint32_t)(ty * L.ntx + tx) * tile_bytes<float>(L);
+    }
+    const int nact = L.visit_stats && entry >= 0 ? __builtin_popcountll(__ballot(ct.fl & C_ACT)) : 0;
+    asm volatile("" ::: "memory");
+    S.meta[ri * 64 + threadIdx.x] = meta;
+    if (threadIdx.x == 0) {
+        if (entry >= 0) {
+            S.lastproc[bid] = (unsigned short)C;
+            if (L.visit_stats) {
+                S.scratch[0] += nbv;
+                S.scratch[1] += nbv * nact;
+            }
+        }
+        S.ring_e[ri] = entry;
+        S.ring_b[ri] = bid;
+        S.ring_base[ri] = base;
+    }
+    asm volatile("" ::: "memory");
+}
+
+// Start of an iteration: every block's pending state (it changed at its last
+// visit, or a face neighbour changed since) becomes lastchg 1 / 0 against
+// lastproc 1, and the clock restarts at 64.  The decisions of the iteration
+// are those of unbounded clocks (all that matters of the past is the
+// pending state; nothing is in flight across an iteration boundary), and an
+// iteration needs at most 8 (nblocks (1 + vis) + infl) + 64 < 2^16 clocks.
+__device__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
+{
+    const int nt = L.ntiles, nzk = L.nzk;
+    unsigned pend = 0;                       // bit i: block lane + 64 i (nblocks <= 1024)
+    for (int i = 0; i * 64 < L.nblocks; i++) {
+        const int b = threadIdx.x + 64 * i;
+        if (b >= L.nblocks) break;
+        const int tz = b / nt, id = b - tz * nt, ty = id / L.ntx, tx = id - ty * L.ntx;
+        const int lp = S.lastproc[b];
+        bool d = S.lastchg[b] >= lp;
+        if (tx > 0) d |= S.lastchg[b - 1] > lp;
+        if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
+        if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
+        if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
+        if (tz > 0) d |= S.lastchg[b - nt] > lp;
+        if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
+        if (d) pend |= 1u << i;
+    }
+    asm volatile("" ::: "memory");
+    for (int i = 0; i * 64 < L.nblocks; i++) {
+        const int b = threadIdx.x + 64 * i;
+        if (b >= L.nblocks) break;
+        S.lastproc[b] = 1;
+        S.lastchg[b] = (pend >> i) & 1u;
+    }
+    asm volatile("" ::: "memory");
+}
+
+// The 16 z-slots of the current brick, updated in place (v).  GENERIC as in
+// fsm_kernel.hip brick_update (grid-edge columns of cut tiles, cut z-bricks,
+// BC nodes, node (0,0,0)); otherwise every lane's missing x/y neighbours are
+// already its own old values (the halo of a grid-edge lane is its column).
+template <bool RZ, bool GENERIC>
+__device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, const BInfo16 &b0, float (&v)[16],
+                                        float zprev0, float znext, int lx, int ly, int rx, int ry, bool &changed,
+                                        bool &nc, int &ierr_last)
+{
+    const int lane = threadIdx.x;
+    const float T = (float)L.conv_thresh;
+    const int fl = b0.fl;
+    bool xp = true, xn = true, yp = true, yn = true, act = true;
+    if (GENERIC) {
+        const int e = S.ring_e[b0.ri];
+        const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
+        const bool xlo = x > 0, xhi = x < L.nx - 1, ylo = y > 0, yhi = y < L.ny - 1;
+        xp = rx ? xhi : xlo; xn = rx ? xlo : xhi; yp = ry ? yhi : ylo; yn = ry ? ylo : yhi;
+        act = (fl & C_ACT) != 0;
+    }
+    const bool first = (fl & F_FIRST) != 0, last = (fl & F_LAST) != 0;
+    const int lxs = lane & 7, lys = lane >> 3;
+    const int rxm = lxs > 0 ? lane - 1 : 64 + lys, rym = lys > 0 ? lane - 8 : 72 + lxs;
+    const int rxp = lxs < 7 ? lane + 1 : 64 + lys, ryp = lys < 7 ? lane + 8 : 72 + lxs;
+    float fc = 0.f, ffc = 0.f, ff2c = 0.f, ff3c = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+        // the half of the brick this pass updates (sweep order: low z first
+        // unless RZ) and the four neighbour rows' values for it
+        const int h = RZ ? 1 - hh : hh;
+        float xm[8], xq[8], ym[8], yq[8];
+        load_half16(S.xr, 0, rxm, h, xm);
+        load_half16(S.xr, 0, rym, h, ym);
+        load_half16(S.xr, 1, rxp, h, xq);
+        load_half16(S.xr, 1, ryp, h, yq);
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const int j = hh * 8 + jj;                      // sweep-order slot
+            const int pj = RZ ? 15 - j : j;                 // z slot
+            const int ph = pj & 7;                          // index in the half
+            const int pprev = RZ ? pj + 1 : pj - 1, pnext = RZ ? pj - 1 : pj + 1;
+            const float self = v[pj];
+            if (!GENERIC) {
+                if (jj == 0 || jj == 4) {                   // a new cell (4 z per cell) in sweep order
+                    fc = S.cc[b0.ccb + (pj >> 2)];
+                    ffc = fc * fc;
+                    ff2c = ffc + ffc;
+                    ff3c = 3.0f * ffc;
+                }
+            }
+            float xup = xm[ph], xdn = xq[ph], yup = ym[ph], ydn = yq[ph];
+            float zup, zdn;
+            if (GENERIC) {
+                xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
+                const int zabs = b0.zb * 16 + pj;
+                const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
+                const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
+                zup = zp_ex ? (j > 0 ? v[pprev] : zprev0) : self;
+                zdn = zn_ex ? (j < 15 ? v[pnext] : znext) : self;
+            } else {
+                zup = j > 0 ? v[pprev] : (first ? self : zprev0);
+                zdn = j < 15 ? v[pnext] : (last ? self : znext);
+            }
+            const float ux = fmin_(xup, xdn), uy = fmin_(yup, ydn), uz = fmin_(zup, zdn);
+            float nv;
+            if (GENERIC) {
+                const int zabs = b0.zb * 16 + pj;
+                const int zc_ = zabs < L.nz ? zabs : L.nz - 1;          // cut brick: clamp the cell
+                const float f = S.cc[b0.ccb - b0.zb * 4 + (zc_ >> 2)];
+                int e;
+                const float ub = godunov_bl<true>(ux, uy, uz, f, e);
+                const bool upd = act && zabs < L.nz && !((b0.bcm >> pj) & 1);
+                nv = upd ? fmin_(self, ub) : self;
+                if ((fl & C_00) && zabs == 0) ierr_last = upd ? e : 0;
+            } else {
+                nv = fmin_(self, godunov_v<true>(ux, uy, uz, fc, ffc, ff2c, ff3c));
+            }
+            const bool dec = nv < self;
+            nc |= dec && self >= T;
+            changed |= dec;
+            v[pj] = nv;
+        }
+    }
+}
+
+// One Gauss-Seidel sweep in direction (rx, ry, RZ) over the admitted
+// z-blocks; returns the stream positions used.  The step structure follows
+// fsm_kernel.hip sweep() (prefetch AH = 2 steps ahead, loads consumed before
+// the step's stores, the next position decided at the end of a step), with
+// 16-z bricks and the brick values updated in place: a lane's next brick
+// lives in its XN row and is read back into v at the end of the step.
+template <bool RZ, int KB16>
+__device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr,
+                                       const BcBoxes &bc, const Smem16 &S, int rx, int ry, int clock0, bool &notconv,
+                                       int &ierr_last, unsigned &nchg)
+{
+    const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
+    const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
+    const float UN = FLT_MAX;
+    const int kb = KB16 > 0 ? KB16 : g.kb;
+    const int nr = KB16 > 0 ? F16_NR : g.nr;
+    const uint32_t lanecol = (uint32_t)colpos(lx, ly) * 128u;
+
+    // halo loader role: half hh of halo column hj (edge lane he, lag hd)
+    const int hj = lane >> 1, hh = lane & 1, he = halo_edge_lane(hj), hd = (he & 7) + (he >> 3);
+    const unsigned hbit = hj < 16 ? C_XOWN : C_YOWN;
+    const uint32_t hdelta = halo_delta(L, tile_bytes<float>(L), hj, he, rx, ry);
+    const int hlx = rx ? 7 - (he & 7) : (he & 7), hly = ry ? 7 - (he >> 3) : (he >> 3);
+    const uint32_t hcol = (uint32_t)colpos(hlx, hly) * 128u;
+
+    Stream st;
+    st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
+    float v[16], qa[16], hq[8], hn[8];
+    float zc, zn, zq;
+    float ccv[1];
+    int ccsize = 0;
+    ColTile ct;
+    ct.tile = -1;
+    // prologue decisions: positions of lane (0,0)'s bricks 0 .. AH-1
+    constexpr int AH = MCEIK_AHEAD16;
+    int ndecided = 0, nstream = 0x7fffffff, dri = 0;
+    for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
+        int zh;
+        const int e = decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
+        if (e == -2) {
+            if (pos == 0) return 0;                         // nothing changed near any block: skip the sweep
+            nstream = pos;
+            break;
+        }
+        admit16(L, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
+        if (e >= 0) {
+            cc_issue<1>(L, L.kb, sr, e, ccv, ccsize);
+            TRAFU(S, 5, ccsize * 4);
+            cc_write<float, 1>(L, S.cc, dri, ccv, ccsize, (float)L.h);
+        }
+        ndecided = pos + 1;
+        if (++dri == nr) dri = 0;
+    }
+    asm volatile("" ::: "memory");
+    // bricks vb (b0) and vb+1 (b1); the loop computes vb+2's (b3) and carries it
+    Pos p3, pe;
+    pos_init(p3, -d, kb, nr);
+    BInfo16 b0 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
+                                  S.ring_base[p3.ri] + lanecol);
+    {
+        float t[16];
+        seg_issue(ur, b0.seg, t);
+        seg_finish(t, v);
+    }
+    pos_init(pe, -hd, kb, nr);
+    {
+        const uint32_t ho = halo_offset16<RZ>(g, pe, nstream, hh, S.meta[pe.ri * 64 + he],
+                                              S.ring_base[pe.ri] + hcol, hbit, hdelta);
+        bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hq[0]));
+        bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hq[4]));
+        TRAF(S, 1, ho != OOB, 32);
+    }
+    zc = bload1(ur, b0.zh, 0.0f);
+    TRAF(S, 0, b0.seg != OOB, 64);
+    TRAF(S, 2, b0.zh != OOB, 4);
+    pos_adv(p3, kb, nr);
+    BInfo16 b1 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
+                                  S.ring_base[p3.ri] + lanecol);
+    {
+        float t[16], n[16];
+        seg_issue(ur, b1.seg, t);
+        seg_finish(t, n);
+        store_row16(S.xr, 1, lane, n);              // brick vb0 + 1: this lane's XN row
+    }
+    pos_adv(pe, kb, nr);
+    {
+        const uint32_t ho = halo_offset16<RZ>(g, pe, nstream, hh, S.meta[pe.ri * 64 + he],
+                                              S.ring_base[pe.ri] + hcol, hbit, hdelta);
+        bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
+        bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
+        TRAF(S, 1, ho != OOB, 32);
+    }
+    zn = bload1(ur, b1.zh, 0.0f);
+    TRAF(S, 0, b1.seg != OOB, 64);
+    TRAF(S, 2, b1.zh != OOB, 4);
+    {
+        float un[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) un[i] = UN;
+        store_row16(S.xr, 0, lane, un);             // no results yet
+    }
+    halo_stage16(S.xr, lane, hq);
+    float zprev = UN;                                // last slot of the previous brick (sweep order)
+#pragma unroll
+    for (int i = 0; i < 8; i++) hq[i] = hn[i];
+    // the prologue's loads are waited for here, once per sweep
+#pragma unroll
+    for (int i = 0; i < 16; i++) asm volatile("" : "+v"(v[i]));
+#pragma unroll
+    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hq[i]));
+    asm volatile("" : "+v"(zc), "+v"(zn));
+    asm volatile("" ::: "memory");
+
+    int ph = AH % kb;
+    int cc_pend = -1;
+    int B = 0;
+    bool ccfill = false;
+    int ccri = 0;
+    auto decide_step = [&]() __attribute__((always_inline)) {
+        ccfill = false;
+        ccri = 0;
+        if (ph == 0 && nstream == 0x7fffffff) {
+            const int pos = ndecided;
+            int zh;
+            const int e = decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
+            if (e == -2) {
+                nstream = pos;
+            } else {
+                admit16(L, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
+                if (e >= 0) {
+                    cc_issue<1>(L, L.kb, sr, e, ccv, ccsize);
+                    TRAFU(S, 5, ccsize * 4);
+                    ccfill = true;
+                    ccri = dri;
+                }
+                ndecided = pos + 1;
+                if (++dri == nr) dri = 0;
+            }
+        }
+    };
+    auto more = [&]() __attribute__((always_inline)) -> bool {
+        return !(nstream != 0x7fffffff && B >= nstream * kb + 14);
+    };
+    auto step = [&]() __attribute__((always_inline)) -> bool {
+        // ---- prefetch: own segment and halos of vb+2 (consumed at the end of
+        // this step, before its stores; halos staged at the end of the next)
+        pos_adv(p3, kb, nr);
+        pos_adv(pe, kb, nr);
+        const unsigned m3 = S.meta[p3.ri * 64 + lane], me = S.meta[pe.ri * 64 + he];
+        const uint32_t c3 = S.ring_base[p3.ri] + lanecol, ce = S.ring_base[pe.ri] + hcol;
+        __builtin_amdgcn_sched_barrier(0);
+        const BInfo16 b3 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, m3, c3);
+        seg_issue(ur, b3.seg, qa);
+        zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
+        {
+            const uint32_t ho = halo_offset16<RZ>(g, pe, nstream, hh, me, ce, hbit, hdelta);
+            bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
+            bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
+            TRAF(S, 1, ho != OOB, 32);
+            TRAF(S, 0, b3.seg != OOB, 64);
+            TRAF(S, 2, b3.zh != OOB, 4);
+        }
+        // ---- u0: old values of a block's first visit in the iteration (< T only)
+        if (__any(b0.fl & C_U0)) {
+            unsigned m = __builtin_bit_cast(unsigned, v[0]);
+#pragma unroll
+            for (int i = 1; i < 16; i++) m = min(m, __builtin_bit_cast(unsigned, v[i]));
+            const bool st0 = __builtin_bit_cast(float, m) < (float)L.conv_thresh && (b0.fl & C_U0);
+            if (__any(st0)) store16_plain(u0r, st0 ? b0.seg : OOB, v);
+            TRAF(S, 4, st0, 64);
+        }
+        // ---- the 16 z-slots of the current brick (next brick's first value
+        // in sweep order from this lane's XN row)
+        const float znext = S.xr[XROW16(1, RZ ? 3 : 0, lane) + (RZ ? 3 : 0)];
+        const float zp0 = (b0.fl & F_ZH) ? zc : zprev;
+        bool changed = false, nc = false;
+        if (__any(b0.fl & F_SLOW))
+            brick16<RZ, true>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
+        else
+            brick16<RZ, false>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
+        const bool val = (b0.fl & F_VALID) != 0;
+        changed = changed && val;
+        notconv |= nc && val;
+        nchg += changed ? 2u : 0u;                   // in 8-z segment equivalents
+
+        // ---- consume this step's loads before any store of the step
+        if (cc_pend >= 0) cc_write<float, 1>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
+        cc_pend = ccfill ? ccri : -1;
+        float nn[16];
+        seg_finish(qa, nn);
+        halo_stage16(S.xr, lane, hq);
+#pragma unroll
+        for (int i = 0; i < 8; i++) hq[i] = hn[i];
+        zc = zn; zn = zq;
+#pragma unroll
+        for (int i = 0; i < 16; i++) asm volatile("" : "+v"(nn[i]));
+        asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]), "+v"(hq[4]), "+v"(hq[5]),
+                     "+v"(hq[6]), "+v"(hq[7]));
+        asm volatile("" : "+v"(zn));
+        asm volatile("" ::: "memory");
+        // ---- rows for the next step: results (XR), then this lane's next
+        // brick back into v and the brick after it into XN
+        store_row16(S.xr, 0, lane, v);
+        zprev = v[RZ ? 0 : 15];
+        if (__any(changed)) seg_store(ur, b0.seg, changed, v);
+        TRAF(S, 3, changed, 64);
+        if (changed) S.lastchg[b0.bid] = (unsigned short)(clock0 + b0.clk);
+        load_row16(S.xr, 1, lane, v);
+        store_row16(S.xr, 1, lane, nn);
+        asm volatile("" ::: "memory");
+        b0 = b1;
+        b1 = b3;
+        if (++ph == kb) ph = 0;
+        B++;
+        decide_step();
+        return more();
+    };
+    decide_step();
+    if (more()) {
+        do {
+        } while (step());
+    }
+    return nstream;
+}
+
+// End-of-iteration check of the nodes below T (only when no node >= T
+// changed): the z-blocks changed in this iteration; u0 was stored at their
+// first visit (fsm_kernel.hip verify_small, 16-bit clocks).
+__device__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem16 &S, bool &notconv)
+{
+    const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
+    const float T = (float)L.conv_thresh, tolr = (float)L.tol;
+    for (int base = 0; base < L.nblocks; base += 64) {
+        const int k = base + lane;
+        const bool flag = k < L.nblocks && S.lastchg[k] >= 64;
+        unsigned long long m = __ballot(flag);
+        while (m) {
+            const int bid = base + __builtin_ctzll(m);
+            m &= m - 1;
+            const int tz = bid / L.ntiles, id = bid - tz * L.ntiles;
+            const int tx = id % L.ntx, ty = id / L.ntx;
+            const int x = tx * 8 + lx, y = ty * 8 + ly;
+            const int zend = min(tz * L.kb + L.kb, L.nzb);
+            for (int zb = tz * L.kb; zb < zend; zb++) {
+                const uint32_t seg = (uint32_t)id * tile_bytes<float>(L) + zoff_bytes<float>(zb) +
+                                     (uint32_t)colpos(lx, ly) * 128u;
+                float u[8], v0[8];
+                bload8(ur, seg, u);
+                bload8(u0r, seg, v0);
+                TRAF(S, 6, x < L.nx && y < L.ny, 64);
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    float dl = v0[i] - u[i];
+                    dl = dl < 0.0f ? -dl : dl;
+                    if (x < L.nx && y < L.ny && zb * 8 + i < L.nz && u[i] < T && !(dl < tolr)) notconv = true;
+                }
+            }
+        }
+    }
+}
+
+template <int KB16>
+__device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Smem16 S = smem16_bind<KB16 == 2>(L, smem);
+    const Fsm16Geo g = fsm16_geo(L);
+    const int lane = threadIdx.x;
+    const uint32_t fbytes = (uint32_t)(L.field_elems * 4);
+    build_order(L, S.order);
+    int pass = 0;
+    for (;;) {
+        const int snext = next_solve(L, pass);
+        if (snext < 0) break;
+        const unsigned solve = (unsigned)snext;
+        if (L.solve_clock && lane == 0) L.solve_clock[2 * (size_t)solve] = __builtin_amdgcn_s_memrealtime();
+        const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
+        const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
+        float *u = reinterpret_cast<float *>(L.u) + slot * L.field_elems;
+        float *u0 = reinterpret_cast<float *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
+        const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
+        const void *slow_model = reinterpret_cast<const float *>(L.slow) + (size_t)model * ncell;
+        const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
+                   sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
+        // Before the first sweep every block counts as visited and unchanged
+        // (lastproc 2 > lastchg 1) except the blocks holding boundary-condition
+        // nodes (lastchg 3): a block whose nodes and neighbours are all u_nan
+        // updates to u_nan, so it needs no visit until a neighbour changes.
+        for (int t = lane; t < L.nblocks; t += 64) {
+            S.lastproc[t] = 2; S.lastchg[t] = 1;
+        }
+        if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
+#ifdef MCEIK_TRAFFIC
+        if (lane == 0)
+            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) S.scratch[8 + k] = 0;
+#endif
+        unsigned nchg = 0;
+        BcBoxes bc;
+        bc.box = S.box;
+        const bool ok = init_field<float, 1>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
+        if (lane == 0) {
+            for (int k = 0; k < bc.n; k++) {
+                const int *q = bc.box + 6 * k;
+                for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
+                    for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
+                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
+                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = 3;
+            }
+        }
+        asm volatile("" ::: "memory");
+        int iters = 0, ierr_last = 0;
+        if (ok) {
+            int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
+            for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
+                bool notconv = false;
+                iter_norm(L, S);
+                int clock = 64;
+                for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
+                    const int rx = sw & 1, ry = (sw >> 1) & 1;
+                    // positions used + a gap of infl: the previous sweep's visits are
+                    // never in flight (nor within vis) for the next one
+                    if (sw & 4)
+                        clock += g.infl + sweep16<true, KB16>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                                                              ierr_last, nchg);
+                    else
+                        clock += g.infl + sweep16<false, KB16>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                                                               ierr_last, nchg);
+                    __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    TRAF_FLUSH(L, S);
+                }
+                iters = it + 1;
+                if (sweeps_left > 0 || L.max_sweeps < 0) {
+                    if (!__any(notconv)) verify16(L, ur, u0r, S, notconv);
+                    if (!__any(notconv)) break;
+                }
+            }
+        }
+        // ierr: from the last evaluation of node (0,0,0) (the reference's last update)
+        int ierr = ierr_last;
+        for (int o = 32; o > 0; o >>= 1) ierr = max(ierr, __shfl_xor(ierr, o, 64));
+        if (!ok) ierr = 1;
+        if (L.visit_stats) {
+            for (int o = 32; o > 0; o >>= 1) nchg += __shfl_xor(nchg, o, 64);
+            asm volatile("" ::: "memory");
+            if (lane == 0) {
+                atomicAdd(L.visit_stats, (unsigned long long)(unsigned)S.scratch[0]);
+                atomicAdd(L.visit_stats + 1, (unsigned long long)(unsigned)S.scratch[1]);
+                atomicAdd(L.visit_stats + 2, (unsigned long long)nchg);
+            }
+        }
+        if (lane == 0) {
+            if (L.solve_clock) L.solve_clock[2 * (size_t)solve + 1] = __builtin_amdgcn_s_memrealtime();
+            if (L.iter_total) atomicAdd(L.iter_total, (unsigned long long)iters);
+            if (L.niter) L.niter[solve] = iters;
+            if (L.ierr) L.ierr[solve] = ierr;
+        }
+        TRAFU(S, 7, (unsigned)(L.field_elems * 4) + (L.ttab ? (unsigned)L.nev * (4u + 64u) : 0u));
+        TRAF_FLUSH(L, S);
+        if (L.ttab) {
+            for (int e = lane; e < L.nev; e += 64) {
+                const int node = L.ev_node[e];
+                const int nxy = L.nx * L.ny;
+                const int z = node / nxy, rem = node - z * nxy, y = rem / L.nx, x = rem - y * L.nx;
+                L.ttab[(size_t)solve * L.nev + e] = u[brick_index<float>(L, x, y, z)];
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+}
+
+// register budget: two waves per SIMD (<= 256 VGPRs)
+#ifndef MCEIK_WPE16
+#define MCEIK_WPE16 2
+#endif
+#define FSM16_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE16, MCEIK_WPE16)))
+template <int KB16>
+__global__ __launch_bounds__(64) FSM16_WPE void fsm16_solve_kernel(FsmLaunch L)
+{
+    fsm16_body<KB16>(L);
+}
+
+}  // namespace
+
+// ---- host-side launchers (used by fsm_kernel.hip's dispatcher) -------------
+hipError_t fsm16_launch(const FsmLaunch &L, int nwaves, hipStream_t st)
+{
+    if (!fsm16_eligible(L, 4)) return hipErrorInvalidValue;
+    const size_t lds = fsm16_lds_bytes(L);
+    if (fsm16_fixed_layout(L))
+        hipLaunchKernelGGL((fsm16_solve_kernel<2>), dim3(nwaves), dim3(64), lds, st, L);
+    else
+        hipLaunchKernelGGL((fsm16_solve_kernel<0>), dim3(nwaves), dim3(64), lds, st, L);
+    return hipGetLastError();
+}
+
+int fsm16_occupancy(const FsmLaunch &L)
+{
+    int nb = 0;
+    const size_t lds = fsm16_lds_bytes(L);
+    const hipError_t e = fsm16_fixed_layout(L)
+                             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<2>, 64, lds)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0>, 64, lds);
+    return e == hipSuccess ? nb : 1;
+}

@@ -53,9 +53,10 @@ struct FsmLaunch {
     unsigned long long *solve_clock;  // [nsolve][2] realtime at solve start / end, or null
     int max_waves;               // host only: cap on resident waves (0 = occupancy x CUs)
     unsigned long long *traffic; // [MCEIK_TRAFFIC_N] requested bytes by category (MCEIK_TRAFFIC builds), or null
+    int step_z;                  // host only: 8 forces the 8-z kernel, 0 = the launch's choice
 };
 
-static inline int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
+static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 
 // Debug / accounting counters in LDS: [0..3] visit statistics; MCEIK_TRAFFIC
 // builds add [8..15], the requested global-memory bytes of the wave's current
@@ -132,6 +133,80 @@ static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)
     return fsm_smem_layout(L, es, off);
 }
 #define MCEIK_MAX_LDS (64 * 1024)   // dynamic LDS without a launch attribute
+
+// ---- 16-z-step kernel (fsm16_kernel.hip, the fp32 cell-cache sampler
+// instance).  A macro step updates 16 z of every lane's column (half of its
+// 128-B line), so a line is consumed in two pieces instead of four.  Stream
+// positions are the same z-blocks: L.kb 8-z bricks = kb/2 steps; L.kb must be
+// even and >= 4 (the 16-bit block clocks below need at most 1 + vis <= 7
+// positions per block and sweep).  Timing rules in steps, as for the 8-z
+// kernel (fsm_geometry): infl = 1 + ceil((14 + AH) / kb16), vis =
+// ceil(12 / kb16), nr = 1 + ceil((15 + AH) / kb16).
+#define MCEIK_AHEAD16 2
+struct Fsm16Geo {
+    int nzb, kb, nr, infl, vis;  // 16-z bricks per column, steps per position, ring, in-flight, visibility
+};
+static inline __host__ __device__ Fsm16Geo fsm16_geo(const FsmLaunch &L)
+{
+    Fsm16Geo g;
+    g.nzb = mceik_div_up(L.nz, 16);
+    g.kb = L.kb / 2;
+    g.infl = 1 + mceik_div_up(14 + MCEIK_AHEAD16, g.kb);
+    g.vis = mceik_div_up(12, g.kb);
+    g.nr = 1 + mceik_div_up(15 + MCEIK_AHEAD16, g.kb);
+    return g;
+}
+static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t es)
+{
+    return es == 4 && L.slow_mode != 0 && L.cell_cache && L.fast_sqrt && L.nrz == 4 && L.ccb <= 64 &&
+           L.kb >= 4 && (L.kb & 1) == 0 && L.nblocks <= MCEIK_MAX_BLOCKS;
+}
+// LDS of one fsm16 solve wave: 0 BC boxes | 1 cell cache [nr][ccb] float | 2 tile order int [ntiles] |
+// 3 lastproc u16 [nblocks] | 4 lastchg u16 [nblocks] (clocks relative to the iteration) |
+// 5 ring: entry int [nr], block id int [nr], tile base u32 [nr] | 6 scratch |
+// 7 neighbour rows XR then XN, each [4 quarters][80 rows][4] float | 8 column meta u32 [nr][64]
+#define MCEIK_SMEM16_ARRAYS 9
+#define F16_NR (1 + (15 + MCEIK_AHEAD16 + 1) / 2)      // nr at kb16 = 2
+#define F16_CINFO 0
+#define F16_XR (F16_CINFO + F16_NR * 64 * 4)
+#define F16_CC (F16_XR + 2 * 4 * MCEIK_XROWS * 16)
+#define F16_RING (F16_CC + F16_NR * 32 * 4)
+#define F16_SCRATCH (F16_RING + 128)
+#define F16_LASTPROC (F16_SCRATCH + MCEIK_SCRATCH_BYTES)
+#define F16_LASTCHG (F16_LASTPROC + MCEIK_MAX_BLOCKS * 2)
+#define F16_ORDER (F16_LASTCHG + MCEIK_MAX_BLOCKS * 2)
+static inline __host__ __device__ bool fsm16_fixed_layout(const FsmLaunch &L)
+{
+    return fsm16_eligible(L, 4) && L.kb == 4 && L.ccb <= 32 && fsm16_geo(L).nr == F16_NR;
+}
+static inline __host__ __device__ size_t fsm16_smem_layout(const FsmLaunch &L, size_t *off)
+{
+    const size_t nbox = mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
+    if (fsm16_fixed_layout(L)) {
+        off[8] = F16_CINFO; off[7] = F16_XR; off[1] = F16_CC; off[5] = F16_RING; off[6] = F16_SCRATCH;
+        off[3] = F16_LASTPROC; off[4] = F16_LASTCHG; off[2] = F16_ORDER;
+        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 4);
+        return off[0] + nbox;
+    }
+    const Fsm16Geo g = fsm16_geo(L);
+    const size_t nr = (size_t)g.nr, nb = (size_t)L.nblocks;
+    size_t o = 0;
+    off[0] = o; o += nbox;
+    off[1] = o; o += mceik_align16(nr * L.ccb * 4);
+    off[2] = o; o += mceik_align16((size_t)L.ntiles * 4);
+    off[3] = o; o += mceik_align16(nb * 2);
+    off[4] = o; o += mceik_align16(nb * 2);
+    off[5] = o; o += mceik_align16(nr * 12);
+    off[6] = o; o += MCEIK_SCRATCH_BYTES;
+    off[7] = o; o += 2 * 4 * MCEIK_XROWS * 16;
+    off[8] = o; o += nr * 64 * 4;
+    return o;
+}
+static inline size_t fsm16_lds_bytes(const FsmLaunch &L)
+{
+    size_t off[MCEIK_SMEM16_ARRAYS];
+    return fsm16_smem_layout(L, off);
+}
 
 // Fills the tile geometry of a launch from nx, ny, nz (es: element bytes).
 // Field layout: per 8x8 column tile, z-major groups of one

@@ -202,7 +202,7 @@ class BatchSolver:
         self.nref = nref
         self._ws = None
 
-    def describe(self, nmodel, nstat, nsrc, slow_mode, nev=0, max_sweeps=-1, max_waves=0):
+    def describe(self, nmodel, nstat, nsrc, slow_mode, nev=0, max_sweeps=-1, max_waves=0, step_z=0):
         b = _lib.FsmBatch()
         b.nx, b.ny, b.nz = self.nx, self.ny, self.nz
         b.h, b.x0, b.y0, b.z0 = self.h, self.x0, self.y0, self.z0
@@ -215,16 +215,20 @@ class BatchSolver:
         b.max_sweeps = max_sweeps
         b.fast_sqrt = 1 if (self.fast_sqrt and slow_mode == 1) else 0
         b.max_waves = int(max_waves)
+        b.step_z = int(step_z)
         return b
 
     def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None,
-              solve_order=None, solve_clock=False, max_waves=0):
+              solve_order=None, solve_clock=False, max_waves=0, step_z=0):
         """solve_order: optional permutation of the nmodel*nstat solve ids (the
         order the work queues hand them out; results do not depend on it).
         solve_clock: also return out["clock"] [nsolve][2], the device realtime
         (100 MHz) at the start and end of every solve.  max_waves: cap on the
         resident solve waves (0 = occupancy x CUs); fewer waves than solves runs
-        the production path (several solves per wave in reused scratch)."""
+        the production path (several solves per wave in reused scratch).
+        step_z: 0 = the launch's kernel (16-z steps for the fp32 cell-cache
+        instance, else 8-z; out["step_z"] says which ran), 8 = force the 8-z
+        kernel; the results are identical."""
         import torch
         dev = slow.device
         sources = sources.to(device=dev, dtype=torch.float64).contiguous()
@@ -238,7 +242,7 @@ class BatchSolver:
             raise TypeError("cell slowness must be float32")
         slow = slow.contiguous()
         nev = 0 if ev_node is None else int(ev_node.numel())
-        b = self.describe(nmodel, nstat, nsrc, slow_mode, nev, max_sweeps, max_waves)
+        b = self.describe(nmodel, nstat, nsrc, slow_mode, nev, max_sweeps, max_waves, step_z)
         nsolve = nmodel * nstat
         niter = torch.zeros(nsolve, dtype=torch.int32, device=dev)
         ierr = torch.zeros(nsolve, dtype=torch.int32, device=dev)
@@ -277,4 +281,5 @@ class BatchSolver:
             raise RuntimeError(f"mceik_fsm_batch_solve failed ({rc})")
         out["_keep"] = (sources, slow)
         out["bytes_per_node_sweep"] = L.mceik_fsm_bytes_per_node_sweep(C.byref(b))
+        out["step_z"] = L.mceik_fsm_step_z(C.byref(b))
         return out

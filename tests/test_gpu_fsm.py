@@ -137,6 +137,8 @@ def test_fp32_inversion_grid_mode_bitwise(fast, nz):
     from mceik_amd.eikonal import BatchSolver
     bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=fast)
     out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(1, -1), device=dev), want_fields=True)
+    # the fast cell-cache instance with even z-blocks runs the 16-z-step kernel
+    assert out["step_z"] == (16 if fast and nz != 20 else 8)
     u = out["u"].cpu().numpy().reshape(2, -1)
     for s in range(2):
         t, _, it = O.eikonal_solve(nx, ny, nz, sfield, h, src[s], dtype=np.float32)
@@ -187,10 +189,46 @@ def test_fp32_inversion_grid_mode_8brick_blocks():
     from mceik_amd.eikonal import BatchSolver
     bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=True)
     out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(1, -1), device=dev), want_fields=True)
+    assert out["step_z"] == 16          # runtime-kb instance of the 16-z-step kernel (kb16 = 4)
     u = out["u"].cpu().numpy().reshape(1, -1)
     t, _, it = O.eikonal_solve(nx, ny, nz, sfield, h, src[0], dtype=np.float32)
     assert np.array_equal(u[0].view(np.uint32), t.view(np.uint32))
     assert int(out["niter"][0]) == it
+
+
+STEP_CASES = [
+    # (name, nx, ny, nz, nmodel, sources per station, max_waves)
+    ("ragged_30x26x67", 30, 26, 67, 2, [(0.0, 1234.5, 987.6, 6600.0), (0.0, 300.0, 2200.0, 6600.0),
+                                        (0.1, 1500.0, 1200.0, 3300.0)], 2),
+    ("c2_64cube_reuse", 64, 64, 64, 2, [(0.0, 3100.5, 2950.2, 6300.0), (0.0, 700.0, 5400.0, 6300.0)], 1),
+    ("tall_24x16x200", 24, 16, 200, 1, [(0.0, 1150.0, 730.0, 19900.0), (0.0, 400.0, 200.0, 10000.0)], 0),
+]
+
+
+@pytest.mark.parametrize("case", STEP_CASES, ids=[c[0] for c in STEP_CASES])
+def test_fsm16_steps_equal_8z_kernel_bitwise(case):
+    """The 16-z-step kernel (fsm16_kernel.hip, the sampler's instance) and the
+    8-z kernel give bitwise the same fields, tables and iteration counts:
+    ragged tiles and a cut last 16-z brick (generic path), sources on nodes
+    and inside the grid, several solves per wave in reused scratch."""
+    name, nx, ny, nz, nmodel, srcs, max_waves = case
+    dev = _dev()
+    h, nref = 100.0, (4, 4, 4)
+    ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
+    rng = np.random.default_rng(17)
+    v = rng.integers(2500, 6500, (nmodel, ncz, ncy, ncx)).astype(np.int32)
+    scell = torch.tensor((1.0 / v.astype(np.float32)).reshape(nmodel, -1), device=dev)
+    src = torch.tensor(np.asarray(srcs, dtype=np.float64)[:, None, :])
+    ev = torch.tensor(rng.integers(0, nx * ny * nz, 9).astype(np.int32))
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=True)
+    a = bs.solve(src, scell, ev_node=ev, want_fields=True, max_waves=max_waves)
+    b = bs.solve(src, scell, ev_node=ev, want_fields=True, max_waves=max_waves, step_z=8)
+    assert (a["step_z"], b["step_z"]) == (16, 8)
+    assert torch.equal(a["u"].view(torch.int32), b["u"].view(torch.int32))
+    assert torch.equal(a["ttab"].view(torch.int32), b["ttab"].view(torch.int32))
+    assert torch.equal(a["niter"], b["niter"]) and torch.equal(a["ierr"], b["ierr"])
+    assert not a["ierr"].any()
 
 
 FSM_FILES = sorted(glob.glob(os.path.join(GOLD, "fsm_*.npz")))
