@@ -125,8 +125,22 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 //   i3: even partner q2, odd own q3           (odd's line)
 // even then holds E0 E2 O0 O2 and odd E1 E3 O1 O3; seg_finish swaps the
 // partner's quarters (DPP quad_perm [1,0,3,2]).
+// MCEIK16_PAIR = 0: every lane loads / stores its own four quarters (each
+// instruction touches 64 lines; no swap VALU)
+#ifndef MCEIK16_PAIR
+#define MCEIK16_PAIR 1
+#endif
 __device__ __forceinline__ void seg_issue(Rsrc r, uint32_t seg, float (&a)[16])
 {
+    if (!MCEIK16_PAIR) {
+        float t[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            bload4(r, seg + 16u * q, t);
+            a[4 * q] = t[0]; a[4 * q + 1] = t[1]; a[4 * q + 2] = t[2]; a[4 * q + 3] = t[3];
+        }
+        return;
+    }
     const bool odd = threadIdx.x & 1;
     const uint32_t segp = dpp_swap_pair(seg);
     float t[4];
@@ -141,6 +155,11 @@ __device__ __forceinline__ void seg_issue(Rsrc r, uint32_t seg, float (&a)[16])
 }
 __device__ __forceinline__ void seg_finish(const float (&a)[16], float (&v)[16])
 {
+    if (!MCEIK16_PAIR) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = a[i];
+        return;
+    }
     const bool odd = threadIdx.x & 1;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -154,9 +173,53 @@ __device__ __forceinline__ void seg_finish(const float (&a)[16], float (&v)[16])
         v[8 * q + 4 + k] = odd ? a[8 + 4 * q + k] : recv;
     }
 }
+// The pair exchange through the neighbour rows instead of DPP swaps (no
+// VALU): the raw quarters of seg_issue are written straight into the rows
+// they belong to -- even lane: own q0, own q2, odd's q0, odd's q2; odd lane:
+// even's q1, even's q3, own q1, own q3, i.e. base pair_row(arr) + {0, 2Q, 4,
+// 2Q + 4} floats -- and a paired store reads its operands back the same way
+// from the XR rows (raw_read), so both lanes of an instruction hit one line.
+#define XQE (MCEIK_XROWS * 4)    // floats per quarter array
+__device__ __forceinline__ int pair_row(int arr, int lane)
+{
+    return (lane & 1) ? XROW16(arr, 1, lane - 1) : XROW16(arr, 0, lane);
+}
+__device__ __forceinline__ void raw_write(float *x, int pb, const float (&a)[16])
+{
+    lds_w4(x + pb, a[0], a[1], a[2], a[3]);
+    lds_w4(x + pb + 2 * XQE, a[4], a[5], a[6], a[7]);
+    lds_w4(x + pb + 4, a[8], a[9], a[10], a[11]);
+    lds_w4(x + pb + 2 * XQE + 4, a[12], a[13], a[14], a[15]);
+}
+__device__ __forceinline__ void raw_read(const float *x, int pb, float (&a)[16])
+{
+    lds_r4(x + pb, a[0], a[1], a[2], a[3]);
+    lds_r4(x + pb + 2 * XQE, a[4], a[5], a[6], a[7]);
+    lds_r4(x + pb + 4, a[8], a[9], a[10], a[11]);
+    lds_r4(x + pb + 2 * XQE + 4, a[12], a[13], a[14], a[15]);
+}
+// paired write-back of changed segments from raw_read operands t
+__device__ __forceinline__ void raw_store(Rsrc r, uint32_t seg, bool chg, const float (&t)[16])
+{
+    const bool odd = threadIdx.x & 1;
+    const uint32_t own = chg ? seg : OOB;
+    const uint32_t oth = dpp_swap_pair(own);
+    const uint32_t o = odd ? 16u : 0u;
+    const uint32_t b01 = (odd ? oth : own) + o, b23 = (odd ? own : oth) + o;
+    bstore4(r, b01, t[0], t[1], t[2], t[3]);
+    bstore4(r, b01 + 32u, t[4], t[5], t[6], t[7]);
+    bstore4(r, b23, t[8], t[9], t[10], t[11]);
+    bstore4(r, b23 + 32u, t[12], t[13], t[14], t[15]);
+}
 // changed segments only: the same pairing for the write-back
 __device__ __forceinline__ void seg_store(Rsrc r, uint32_t seg, bool chg, const float (&v)[16])
 {
+    if (!MCEIK16_PAIR) {
+        const uint32_t own = chg ? seg : OOB;
+#pragma unroll
+        for (int q = 0; q < 4; q++) bstore4(r, own + 16u * q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        return;
+    }
     const bool odd = threadIdx.x & 1;
     const uint32_t own = chg ? seg : OOB;
     const uint32_t oth = dpp_swap_pair(own);
@@ -534,10 +597,16 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     pos_init(p3, -d, kb, nr);
     BInfo16 b0 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
                                   S.ring_base[p3.ri] + lanecol);
+    const int pbr = pair_row(0, lane), pbn = pair_row(1, lane);
     {
         float t[16];
         seg_issue(ur, b0.seg, t);
-        seg_finish(t, v);
+        if (MCEIK16_PAIR) {                           // through this lane's XN row
+            raw_write(S.xr, pbn, t);
+            load_row16(S.xr, 1, lane, v);
+        } else {
+            seg_finish(t, v);
+        }
     }
     pos_init(pe, -hd, kb, nr);
     {
@@ -554,10 +623,15 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     BInfo16 b1 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
                                   S.ring_base[p3.ri] + lanecol);
     {
-        float t[16], n[16];
+        float t[16];
         seg_issue(ur, b1.seg, t);
-        seg_finish(t, n);
-        store_row16(S.xr, 1, lane, n);              // brick vb0 + 1: this lane's XN row
+        if (MCEIK16_PAIR) {
+            raw_write(S.xr, pbn, t);                    // brick vb0 + 1: the XN rows
+        } else {
+            float n[16];
+            seg_finish(t, n);
+            store_row16(S.xr, 1, lane, n);
+        }
     }
     pos_adv(pe, kb, nr);
     {
@@ -664,7 +738,12 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         if (cc_pend >= 0) cc_write<float, 1>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
         cc_pend = ccfill ? ccri : -1;
         float nn[16];
-        seg_finish(qa, nn);
+        if (MCEIK16_PAIR) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) nn[i] = qa[i];     // raw quarters (raw_write below)
+        } else {
+            seg_finish(qa, nn);
+        }
         halo_stage16(S.xr, lane, hq);
 #pragma unroll
         for (int i = 0; i < 8; i++) hq[i] = hn[i];
@@ -679,11 +758,22 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         // brick back into v and the brick after it into XN
         store_row16(S.xr, 0, lane, v);
         zprev = v[RZ ? 0 : 15];
-        if (__any(changed)) seg_store(ur, b0.seg, changed, v);
+        if (__any(changed)) {
+            if (MCEIK16_PAIR) {
+                float t[16];
+                raw_read(S.xr, pbr, t);
+                raw_store(ur, b0.seg, changed, t);
+            } else {
+                seg_store(ur, b0.seg, changed, v);
+            }
+        }
         TRAF(S, 3, changed, 64);
         if (changed) S.lastchg[b0.bid] = (unsigned short)(clock0 + b0.clk);
         load_row16(S.xr, 1, lane, v);
-        store_row16(S.xr, 1, lane, nn);
+        if (MCEIK16_PAIR)
+            raw_write(S.xr, pbn, nn);
+        else
+            store_row16(S.xr, 1, lane, nn);
         asm volatile("" ::: "memory");
         b0 = b1;
         b1 = b3;
