@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t zoff16(int zb)
 struct Smem16 {
     int *box;                    // BC boxes [nsrc][6]
     float *cc;                   // cell cache [nr][ccb] (f = s*h)
-    int *order;                  // diagonal tile order: txs | tys << 16
+    unsigned short *order;       // diagonal tile order: txs | tys << 8 (ntx, nty <= 256)
     unsigned short *lastproc;    // per z-block clock (relative to the iteration) of the last visit
     unsigned short *lastchg;     //   ... of the last visit that changed it
     int *ring_e, *ring_b;        // per position (mod nr): entry tx | ty << 12 | tz << 24 (bubble -1), block id
@@ -57,7 +57,7 @@ __device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char 
     if (FIXED) {         // fsm16_fixed_layout(): constants (checked on the host)
         off[8] = F16_CINFO; off[7] = F16_XR; off[1] = F16_CC; off[5] = F16_RING; off[6] = F16_SCRATCH;
         off[3] = F16_LASTPROC; off[4] = F16_LASTCHG; off[2] = F16_ORDER;
-        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 4);
+        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 2);
     } else {
         fsm16_smem_layout(L, off);
     }
@@ -65,7 +65,7 @@ __device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char 
     Smem16 S;
     S.box = reinterpret_cast<int *>(base + off[0]);
     S.cc = reinterpret_cast<float *>(base + off[1]);
-    S.order = reinterpret_cast<int *>(base + off[2]);
+    S.order = reinterpret_cast<unsigned short *>(base + off[2]);
     S.lastproc = reinterpret_cast<unsigned short *>(base + off[3]);
     S.lastchg = reinterpret_cast<unsigned short *>(base + off[4]);
     S.ring_e = reinterpret_cast<int *>(base + off[5]);
@@ -253,13 +253,13 @@ struct BInfo16 {
     int zb, fl, ccb, ri, bid, clk, bcm;
 };
 template <bool RZ>
-__device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, const Pos &p,
-                                                int nstream, int lx, int ly, const BcBoxes &bc, unsigned meta,
-                                                uint32_t col)
+__device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16Geo &g, int kb, const Smem16 &S,
+                                                const Pos &p, int nstream, int lx, int ly, const BcBoxes &bc,
+                                                unsigned meta, uint32_t col)
 {
     BInfo16 b;
     const int tz = ci_tz(meta);
-    const int zb = tz * g.kb + (RZ ? g.kb - 1 - p.zbs : p.zbs);
+    const int zb = tz * kb + (RZ ? kb - 1 - p.zbs : p.zbs);   // kb: compile-time in the fixed instance
     const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < g.nzb;
     b.seg = valid ? col + zoff16(zb) : OOB;
     const int zu = RZ ? zb * 16 + 16 : zb * 16 - 1;          // z-upwind node of the brick's first slot
@@ -299,13 +299,27 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
 }
 // this lane's half (8 z) of halo column j at the edge lane's position pe
 template <bool RZ>
-__device__ __forceinline__ uint32_t halo_offset16(const Fsm16Geo &g, const Pos &pe, int nstream, int half,
+__device__ __forceinline__ uint32_t halo_offset16(const Fsm16Geo &g, int kb, const Pos &pe, int nstream, int half,
                                                   unsigned meta, uint32_t col, unsigned hbit, uint32_t hdelta)
 {
-    const int zb = ci_tz(meta) * g.kb + (RZ ? g.kb - 1 - pe.zbs : pe.zbs);
+    const int zb = ci_tz(meta) * kb + (RZ ? kb - 1 - pe.zbs : pe.zbs);
     const bool valid = pos_valid(pe, nstream) && (meta & C_BLK) && zb < g.nzb;
     const uint32_t base = col + ((meta & hbit) ? 0u : hdelta);
     return valid ? base + zoff16(zb) + (uint32_t)half * 32u : OOB;
+}
+
+// Diagonal order of the tiles for the (+x, +y) sweep (build_order in
+// fsm_device.h, 16-bit entries txs | tys << 8).
+__device__ void build_order16(const FsmLaunch &L, unsigned short *order)
+{
+    for (int id = threadIdx.x; id < L.ntiles; id += 64) {
+        const int txs = id % L.ntx, tys = id / L.ntx, dg = txs + tys;
+        int rank = 0;
+        for (int e = 0; e < dg; e++)
+            rank += min(e, L.nty - 1) - max(0, e - L.ntx + 1) + 1;
+        rank += tys - max(0, dg - L.ntx + 1);
+        order[rank] = (unsigned short)(txs | (tys << 8));
+    }
 }
 
 // ---- stream decisions (as decide() in fsm_kernel.hip, 16-bit clocks) -----
@@ -322,7 +336,7 @@ __device__ __forceinline__ int decide16(const FsmLaunch &L, const Fsm16Geo &g, c
             int k0 = nzk, entry = 0;
             if (k < nt) {
                 const int o = S.order[k];
-                const int txs = o & 0xffff, tys = o >> 16;
+                const int txs = o & 0xff, tys = o >> 8;
                 const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
                 const int id = ty * L.ntx + tx;
                 const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
@@ -544,7 +558,7 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
 // the step's stores, the next position decided at the end of a step), with
 // 16-z bricks and the brick values updated in place: a lane's next brick
 // lives in its XN row and is read back into v at the end of the step.
-template <bool RZ, int KB16>
+template <bool RZ, int KB16, int CCR>
 __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr,
                                        const BcBoxes &bc, const Smem16 &S, int rx, int ry, int clock0, bool &notconv,
                                        int &ierr_last, unsigned &nchg)
@@ -567,7 +581,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     float v[16], qa[16], hq[8], hn[8];
     float zc, zn, zq;
-    float ccv[1];
+    float ccv[CCR];
     int ccsize = 0;
     ColTile ct;
     ct.tile = -1;
@@ -584,9 +598,9 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         }
         admit16(L, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
         if (e >= 0) {
-            cc_issue<1>(L, L.kb, sr, e, ccv, ccsize);
+            cc_issue<CCR>(L, L.kb, sr, e, ccv, ccsize);
             TRAFU(S, 5, ccsize * 4);
-            cc_write<float, 1>(L, S.cc, dri, ccv, ccsize, (float)L.h);
+            cc_write<float, CCR>(L, S.cc, dri, ccv, ccsize, (float)L.h);
         }
         ndecided = pos + 1;
         if (++dri == nr) dri = 0;
@@ -595,7 +609,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     // bricks vb (b0) and vb+1 (b1); the loop computes vb+2's (b3) and carries it
     Pos p3, pe;
     pos_init(p3, -d, kb, nr);
-    BInfo16 b0 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
+    BInfo16 b0 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
                                   S.ring_base[p3.ri] + lanecol);
     const int pbr = pair_row(0, lane), pbn = pair_row(1, lane);
     {
@@ -610,7 +624,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     }
     pos_init(pe, -hd, kb, nr);
     {
-        const uint32_t ho = halo_offset16<RZ>(g, pe, nstream, hh, S.meta[pe.ri * 64 + he],
+        const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
         bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hq[0]));
         bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hq[4]));
@@ -620,7 +634,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     TRAF(S, 0, b0.seg != OOB, 64);
     TRAF(S, 2, b0.zh != OOB, 4);
     pos_adv(p3, kb, nr);
-    BInfo16 b1 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
+    BInfo16 b1 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
                                   S.ring_base[p3.ri] + lanecol);
     {
         float t[16];
@@ -635,7 +649,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     }
     pos_adv(pe, kb, nr);
     {
-        const uint32_t ho = halo_offset16<RZ>(g, pe, nstream, hh, S.meta[pe.ri * 64 + he],
+        const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
         bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
         bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
@@ -679,7 +693,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             } else {
                 admit16(L, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
                 if (e >= 0) {
-                    cc_issue<1>(L, L.kb, sr, e, ccv, ccsize);
+                    cc_issue<CCR>(L, L.kb, sr, e, ccv, ccsize);
                     TRAFU(S, 5, ccsize * 4);
                     ccfill = true;
                     ccri = dri;
@@ -700,11 +714,11 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         const unsigned m3 = S.meta[p3.ri * 64 + lane], me = S.meta[pe.ri * 64 + he];
         const uint32_t c3 = S.ring_base[p3.ri] + lanecol, ce = S.ring_base[pe.ri] + hcol;
         __builtin_amdgcn_sched_barrier(0);
-        const BInfo16 b3 = brick_info16<RZ>(L, g, S, p3, nstream, lx, ly, bc, m3, c3);
+        const BInfo16 b3 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, m3, c3);
         seg_issue(ur, b3.seg, qa);
         zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
         {
-            const uint32_t ho = halo_offset16<RZ>(g, pe, nstream, hh, me, ce, hbit, hdelta);
+            const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
             bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
             bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
             TRAF(S, 1, ho != OOB, 32);
@@ -735,7 +749,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         nchg += changed ? 2u : 0u;                   // in 8-z segment equivalents
 
         // ---- consume this step's loads before any store of the step
-        if (cc_pend >= 0) cc_write<float, 1>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
+        if (cc_pend >= 0) cc_write<float, CCR>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
         cc_pend = ccfill ? ccri : -1;
         float nn[16];
         if (MCEIK16_PAIR) {
@@ -826,7 +840,7 @@ __device__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem16 &S,
     }
 }
 
-template <int KB16>
+template <int KB16, int CCR>
 __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -834,7 +848,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
     const Fsm16Geo g = fsm16_geo(L);
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * 4);
-    build_order(L, S.order);
+    build_order16(L, S.order);
     int pass = 0;
     for (;;) {
         const int snext = next_solve(L, pass);
@@ -887,10 +901,10 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
                     // positions used + a gap of infl: the previous sweep's visits are
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
-                        clock += g.infl + sweep16<true, KB16>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                        clock += g.infl + sweep16<true, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
                                                               ierr_last, nchg);
                     else
-                        clock += g.infl + sweep16<false, KB16>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                        clock += g.infl + sweep16<false, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
                                                                ierr_last, nchg);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -942,23 +956,27 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
 #define MCEIK_WPE16 2
 #endif
 #define FSM16_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE16, MCEIK_WPE16)))
-template <int KB16>
+template <int KB16, int CCR>
 __global__ __launch_bounds__(64) FSM16_WPE void fsm16_solve_kernel(FsmLaunch L)
 {
-    fsm16_body<KB16>(L);
+    fsm16_body<KB16, CCR>(L);
 }
 
 }  // namespace
 
 // ---- host-side launchers (used by fsm_kernel.hip's dispatcher) -------------
+// instances: <2, 1> the fixed layout (kb16 = 2, <= 32 cells per z-block: C2,
+// C3), <0, 1> runtime kb with <= 64 cells per block, <0, 4> up to 256 (C5)
 hipError_t fsm16_launch(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     if (!fsm16_eligible(L, 4)) return hipErrorInvalidValue;
     const size_t lds = fsm16_lds_bytes(L);
     if (fsm16_fixed_layout(L))
-        hipLaunchKernelGGL((fsm16_solve_kernel<2>), dim3(nwaves), dim3(64), lds, st, L);
+        hipLaunchKernelGGL((fsm16_solve_kernel<2, 1>), dim3(nwaves), dim3(64), lds, st, L);
+    else if (L.ccb <= 64)
+        hipLaunchKernelGGL((fsm16_solve_kernel<0, 1>), dim3(nwaves), dim3(64), lds, st, L);
     else
-        hipLaunchKernelGGL((fsm16_solve_kernel<0>), dim3(nwaves), dim3(64), lds, st, L);
+        hipLaunchKernelGGL((fsm16_solve_kernel<0, 4>), dim3(nwaves), dim3(64), lds, st, L);
     return hipGetLastError();
 }
 
@@ -966,8 +984,12 @@ int fsm16_occupancy(const FsmLaunch &L)
 {
     int nb = 0;
     const size_t lds = fsm16_lds_bytes(L);
-    const hipError_t e = fsm16_fixed_layout(L)
-                             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<2>, 64, lds)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0>, 64, lds);
+    hipError_t e;
+    if (fsm16_fixed_layout(L))
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<2, 1>, 64, lds);
+    else if (L.ccb <= 64)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0, 1>, 64, lds);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0, 4>, 64, lds);
     return e == hipSuccess ? nb : 1;
 }

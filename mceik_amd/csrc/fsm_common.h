@@ -158,11 +158,12 @@ static inline __host__ __device__ Fsm16Geo fsm16_geo(const FsmLaunch &L)
 }
 static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t es)
 {
-    return es == 4 && L.slow_mode != 0 && L.cell_cache && L.fast_sqrt && L.nrz == 4 && L.ccb <= 64 &&
-           L.kb >= 4 && (L.kb & 1) == 0 && L.nblocks <= MCEIK_MAX_BLOCKS;
+    return es == 4 && L.slow_mode != 0 && L.cell_cache && L.fast_sqrt && L.nrz == 4 && L.ccb <= MCEIK_CC_MAX &&
+           L.kb >= 4 && (L.kb & 1) == 0 && L.nblocks <= MCEIK_MAX_BLOCKS && L.ntx <= 256 && L.nty <= 256;
 }
 // LDS of one fsm16 solve wave: 0 BC boxes | 1 cell cache [nr][ccb] float | 2 tile order int [ntiles] |
-// 3 lastproc u16 [nblocks] | 4 lastchg u16 [nblocks] (clocks relative to the iteration) |
+// 2 is u16 (txs | tys << 8) | 3 lastproc u16 [nblocks] | 4 lastchg u16 [nblocks] (clocks relative to the
+// iteration) |
 // 5 ring: entry int [nr], block id int [nr], tile base u32 [nr] | 6 scratch |
 // 7 neighbour rows XR then XN, each [4 quarters][80 rows][4] float | 8 column meta u32 [nr][64]
 #define MCEIK_SMEM16_ARRAYS 9
@@ -185,7 +186,7 @@ static inline __host__ __device__ size_t fsm16_smem_layout(const FsmLaunch &L, s
     if (fsm16_fixed_layout(L)) {
         off[8] = F16_CINFO; off[7] = F16_XR; off[1] = F16_CC; off[5] = F16_RING; off[6] = F16_SCRATCH;
         off[3] = F16_LASTPROC; off[4] = F16_LASTCHG; off[2] = F16_ORDER;
-        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 4);
+        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 2);
         return off[0] + nbox;
     }
     const Fsm16Geo g = fsm16_geo(L);
@@ -193,7 +194,7 @@ static inline __host__ __device__ size_t fsm16_smem_layout(const FsmLaunch &L, s
     size_t o = 0;
     off[0] = o; o += nbox;
     off[1] = o; o += mceik_align16(nr * L.ccb * 4);
-    off[2] = o; o += mceik_align16((size_t)L.ntiles * 4);
+    off[2] = o; o += mceik_align16((size_t)L.ntiles * 2);
     off[3] = o; o += mceik_align16(nb * 2);
     off[4] = o; o += mceik_align16(nb * 2);
     off[5] = o; o += mceik_align16(nr * 12);

@@ -1121,7 +1121,7 @@ static bool use_fsm16(const FsmLaunch &L, int is_double)
 {
     static const bool on = [] { const char *e = getenv("MCEIK_FSM16"); return !(e && e[0] == '0'); }();
     const int v = variant(L, is_double);
-    return on && L.step_z != 8 && (v == 7 || v == 8) && fsm16_eligible(L, 4);
+    return on && L.step_z != 8 && (v == 5 || v == 7 || v == 8) && fsm16_eligible(L, 4);
 }
 size_t fsm_launch_lds_bytes(const FsmLaunch &L, int is_double)
 {

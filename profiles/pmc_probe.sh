@@ -20,7 +20,7 @@ i=0
 for P in "${PASSES[@]}"; do
   i=$((i+1))
   if [ -n "$SEL" ] && [[ " $SEL " != *" $i "* ]]; then continue; fi
-  timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex fsm_solve_kernel -d "$OUT/pass$i" -o pmc --output-format csv -- \
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex "${KREGEX:-fsm16_solve_kernel}" -d "$OUT/pass$i" -o pmc --output-format csv -- \
       python3 bench.py "$@" > "$OUT/bench_pass$i.log" 2>&1
 done
 find "$OUT" -name '*counter_collection.csv'

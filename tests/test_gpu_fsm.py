@@ -202,6 +202,8 @@ STEP_CASES = [
                                         (0.1, 1500.0, 1200.0, 3300.0)], 2),
     ("c2_64cube_reuse", 64, 64, 64, 2, [(0.0, 3100.5, 2950.2, 6300.0), (0.0, 700.0, 5400.0, 6300.0)], 1),
     ("tall_24x16x200", 24, 16, 200, 1, [(0.0, 1150.0, 730.0, 19900.0), (0.0, 400.0, 200.0, 10000.0)], 0),
+    # 1024 tiles: 16-brick z-blocks with 128 cells each (the C5 instance's cell cache of 4 per lane)
+    ("cells128_256x256x128", 256, 256, 128, 1, [(0.0, 12345.6, 6789.0, 12700.0), (0.0, 900.0, 24000.0, 12700.0)], 0),
 ]
 
 
