@@ -205,6 +205,13 @@ def main():
         b = _lib.FsmBatch(); b.precision = 32; b.slow_mode = 1; b.nstat = p.nstat
         b.nrx, b.nry, b.nrz = p.nref
         bpn = _lib.lib().mceik_fsm_bytes_per_node_sweep(C.byref(b))
+        # the instance the sampler launches (same batch geometry as mceik_mcmc_init)
+        b.nx, b.ny, b.nz, b.h = p.nx, p.ny, p.nz, p.h
+        b.nmodel, b.nsrc, b.fast_sqrt, b.maxit, b.tol = per_gpu, 1, 1, p.maxit, p.tol
+        b.nev = p.nevents
+        step_z = _lib.lib().mceik_fsm_step_z(C.byref(b))
+        kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
+                 "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)")
         # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
         # inputs did not change since their last visit are skipped)
         nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
@@ -240,7 +247,7 @@ def main():
                        "stations": p.nstat, "events": p.nevents, "parallelism": f"chains sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "fsm_solve_kernel<float, 2, true, 2, 1, 4> (cells via LDS cache, fast sqrt, nrz=4)",
+                         "kernel": kname,
                          "kernel_rev": KERNEL_REV,
                          "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
                          "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),

@@ -32,6 +32,9 @@ typedef struct mceik_mcmc_opts {
     int precision;             /* FSM arithmetic: 32 (0 = default) or 64; tables are fp32 at rest
                                   either way (fsm3d.f90:1855-1875)           */
     int max_waves;             /* cap on resident FSM waves (0 = occupancy x CUs) */
+    int tt_interp;             /* event travel times: 0 = value at the event's nearest node (the
+                                  reference's snapping, fsm3d.f90:697-711); 1 = trilinear
+                                  interpolation in the event's grid cell (mceik_fsm_batch.ev_frac) */
 } mceik_mcmc_opts;
 
 /* v0: host [nchains][ncell] int m/s, ncell = ceil(nx/nrefx)*ceil(ny/nrefy)*

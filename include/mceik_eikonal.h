@@ -143,6 +143,10 @@ typedef struct mceik_fsm_batch {
     int step_z;                 /* z nodes per macro step of the sweep kernel: 0 = the launch's choice
                                    (16 for the fp32 cell-cache instance, else 8), 8 = force the 8-z
                                    kernel (A/B measurements, parity tests); results are identical */
+    const float *ev_frac;       /* device [nev][3] (wx, wy, wz) in [0, 1], or NULL.  NULL: ttab holds the
+                                   value at node ev_node (the reference's nearest-node snapping,
+                                   fsm3d.f90:697-711).  Else trilinear interpolation in the cell whose
+                                   lowest corner is ev_node (fp32, x then y then z, a + w*(b - a)) */
 } mceik_fsm_batch;
 
 /* Device workspace (bytes) a launch of this batch needs. */

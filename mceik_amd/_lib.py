@@ -24,7 +24,8 @@ class FsmBatch(C.Structure):
                 ("u_out", C.c_void_p), ("niter", C.c_void_p), ("ierr", C.c_void_p),
                 ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
                 ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p),
-                ("max_waves", C.c_int), ("traffic", C.c_void_p), ("step_z", C.c_int)]
+                ("max_waves", C.c_int), ("traffic", C.c_void_p), ("step_z", C.c_int),
+                ("ev_frac", C.c_void_p)]
 
 
 class RelocateBatch(C.Structure):
@@ -73,7 +74,7 @@ class McmcOpts(C.Structure):
     _fields_ = [("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nchains", C.c_int),
                 ("chain_offset", C.c_int), ("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int),
                 ("seed", C.c_uint32), ("max_samples", C.c_int), ("device", C.c_int),
-                ("precision", C.c_int), ("max_waves", C.c_int)]
+                ("precision", C.c_int), ("max_waves", C.c_int), ("tt_interp", C.c_int)]
 
 
 # every extern "C" symbol include/*.h declares

@@ -90,7 +90,7 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.magic_rx = ((1u << 20) + L.nrx - 1) / L.nrx;
     L.magic_ry = ((1u << 20) + L.nry - 1) / L.nry;
     L.magic_rz = ((1u << 20) + L.nrz - 1) / L.nrz;
-    L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab;
+    L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab; L.ev_frac = b->ev_frac;
     // LDS cell cache when every z-block's cells fit (2 x 2 x 8 at nref = 4, kb = 4)
     {
         auto span = [](int a, int e, int nr) { return e / nr - a / nr + 1; };
@@ -870,6 +870,23 @@ static int source_index(int n, double x0, double dx, double xs)   // fsm3d.f90:6
     return (int)((xs - x0) / dx + 0.5);
 }
 
+// Trilinear mode (mceik_mcmc_opts.tt_interp; no reference counterpart): the
+// lowest corner i of the grid cell holding xs, clamped to [0, n-2], and the
+// fraction w = (xs - x0)/dx - i in [0, 1] rounded once to fp32.  Positions
+// outside the grid clamp to its faces (w = 0 or 1), the snapping rule's
+// clamping (fsm3d.f90:697-711).
+static int cell_corner(int n, double x0, double dx, double xs, float *w)
+{
+    if (n < 2) { *w = 0.0f; return 0; }
+    const double f = (xs - x0) / dx;
+    int i = f <= 0.0 ? 0 : (int)f;
+    if (i > n - 2) i = n - 2;
+    double r = f - (double)i;
+    r = r < 0.0 ? 0.0 : (r > 1.0 ? 1.0 : r);
+    *w = (float)r;
+    return i;
+}
+
 // Adds the elapsed time of timed launch k (its pair is complete once its end
 // event is) to fsm_ms.  Blocks only when MCEIK_EV_RING launches are queued.
 static int fold_launch(mceik_mcmc *s, long long k)
@@ -981,10 +998,18 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         src[i * 4 + 0] = 0.0; src[i * 4 + 1] = st->xrec[i]; src[i * 4 + 2] = st->yrec[i]; src[i * 4 + 3] = st->zrec[i];
     }
     std::vector<int> ev(nev);
+    std::vector<float> evf(o->tt_interp ? (size_t)nev * 3 : 0);
     for (int e = 0; e < nev; e++) {
-        int ix = source_index(o->nx, parms->x0, parms->dx, cat->xsrc[e]);
-        int iy = source_index(o->ny, parms->y0, parms->dx, cat->ysrc[e]);
-        int iz = source_index(o->nz, parms->z0, parms->dx, cat->zsrc[e]);
+        int ix, iy, iz;
+        if (o->tt_interp) {   // lowest corner of the event's cell + fractions (trilinear mode)
+            ix = cell_corner(o->nx, parms->x0, parms->dx, cat->xsrc[e], &evf[3 * e]);
+            iy = cell_corner(o->ny, parms->y0, parms->dx, cat->ysrc[e], &evf[3 * e + 1]);
+            iz = cell_corner(o->nz, parms->z0, parms->dx, cat->zsrc[e], &evf[3 * e + 2]);
+        } else {
+            ix = source_index(o->nx, parms->x0, parms->dx, cat->xsrc[e]);
+            iy = source_index(o->ny, parms->y0, parms->dx, cat->ysrc[e]);
+            iz = source_index(o->nz, parms->z0, parms->dx, cat->zsrc[e]);
+        }
         ev[e] = (iz * o->ny + iy) * o->nx + ix;
     }
     int nobs = cat->obsPtr[nev];
@@ -1006,6 +1031,8 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     int *d_niter = nullptr;
     rc |= dput(s, &d_src, src.data(), src.size());
     rc |= dput(s, &d_ev, ev.data(), ev.size());
+    float *d_evf = nullptr;
+    if (o->tt_interp) rc |= dput(s, &d_evf, evf.data(), evf.size());
     rc |= dput(s, &d_optr, (const int *)cat->obsPtr, (size_t)nev + 1);
     int *d_ostat = nullptr, *d_omask = nullptr;
     double *d_tobs = nullptr, *d_tcorr = nullptr, *d_var = nullptr;
@@ -1043,7 +1070,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.precision = o->precision == 64 ? 64 : 32;
     b.nmodel = nch; b.nstat = nstat; b.nsrc = 1; b.src = d_src;
     b.slow_mode = 1; b.slow = D.slow_prop; b.nrx = nrx; b.nry = nry; b.nrz = nrz;
-    b.nev = nev; b.ev_node = d_ev; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = s->d_ierr;
+    b.nev = nev; b.ev_node = d_ev; b.ev_frac = d_evf; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = s->d_ierr;
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
     b.visit_stats = s->d_iters + 1;

@@ -939,12 +939,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         TRAFU(S, 7, (unsigned)(L.field_elems * 4) + (L.ttab ? (unsigned)L.nev * (4u + 64u) : 0u));
         TRAF_FLUSH(L, S);
         if (L.ttab) {
-            for (int e = lane; e < L.nev; e += 64) {
-                const int node = L.ev_node[e];
-                const int nxy = L.nx * L.ny;
-                const int z = node / nxy, rem = node - z * nxy, y = rem / L.nx, x = rem - y * L.nx;
-                L.ttab[(size_t)solve * L.nev + e] = u[brick_index<float>(L, x, y, z)];
-            }
+            for (int e = lane; e < L.nev; e += 64) L.ttab[(size_t)solve * L.nev + e] = event_time<float>(L, u, e);
         }
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

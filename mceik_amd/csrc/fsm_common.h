@@ -54,6 +54,7 @@ struct FsmLaunch {
     int max_waves;               // host only: cap on resident waves (0 = occupancy x CUs)
     unsigned long long *traffic; // [MCEIK_TRAFFIC_N] requested bytes by category (MCEIK_TRAFFIC builds), or null
     int step_z;                  // host only: 8 forces the 8-z kernel, 0 = the launch's choice
+    const float *ev_frac;        // [nev][3] trilinear fractions (ev_node = lowest corner), or null = node value
 };
 
 static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b - 1) / b; }

@@ -128,6 +128,34 @@ __device__ __forceinline__ size_t brick_index(const FsmLaunch &L, int x, int y, 
     return (((size_t)tile * L.nzq + z / ZQ) * 64 + colpos(x & 7, y & 7)) * ZQ + z % ZQ;
 }
 
+// Travel time of event e from a finished field (fp32 table value).  ev_frac ==
+// nullptr: the value at node ev_node[e] (the reference snaps sources to the
+// nearest node, fsm3d.f90:697-711).  Otherwise trilinear interpolation in the
+// cell whose lowest corner is ev_node[e], with fractions ev_frac[3e..3e+2]:
+// x first, then y, then z, each lerp a + w*(b - a) in fp32 with every
+// operation rounded (no contraction) -- oracle/mceik_oracle.c
+// oracle_event_time restates it operation for operation.
+template <typename R>
+__device__ __forceinline__ float event_time(const FsmLaunch &L, const R *u, int e)
+{
+    const int node = L.ev_node[e];
+    const int nxy = L.nx * L.ny;
+    const int z = node / nxy, rem = node - z * nxy, y = rem / L.nx, x = rem - y * L.nx;
+    if (!L.ev_frac) return (float)u[brick_index<R>(L, x, y, z)];
+    const float wx = L.ev_frac[3 * e], wy = L.ev_frac[3 * e + 1], wz = L.ev_frac[3 * e + 2];
+    const int x1 = min(x + 1, L.nx - 1), y1 = min(y + 1, L.ny - 1), z1 = min(z + 1, L.nz - 1);
+    float c[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        c[k] = (float)u[brick_index<R>(L, (k & 1) ? x1 : x, (k & 2) ? y1 : y, (k & 4) ? z1 : z)];
+    float a[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) a[k] = __fadd_rn(c[2 * k], __fmul_rn(wx, __fsub_rn(c[2 * k + 1], c[2 * k])));
+    const float b0 = __fadd_rn(a[0], __fmul_rn(wy, __fsub_rn(a[1], a[0])));
+    const float b1 = __fadd_rn(a[2], __fmul_rn(wy, __fsub_rn(a[3], a[2])));
+    return __fadd_rn(b0, __fmul_rn(wz, __fsub_rn(b1, b0)));
+}
+
 // Per-solve boundary-condition boxes (EIKONAL3D_SETBCS nodes, lupd = .FALSE.).
 // Wave-uniform, kept in LDS: box k = {xlo, xhi, ylo, yhi, zlo, zhi} (0-based, inclusive).
 struct BcBoxes {

@@ -1023,12 +1023,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         TRAFU(S, 7, (unsigned)(L.field_elems * sizeof(R)) + (L.ttab ? (unsigned)L.nev * (4u + 64u) : 0u));
         TRAF_FLUSH(L, S);
         if (L.ttab) {
-            for (int e = lane; e < L.nev; e += 64) {
-                int node = L.ev_node[e];
-                int nxy = L.nx * L.ny;
-                int z = node / nxy, rem = node - z * nxy, y = rem / L.nx, x = rem - y * L.nx;
-                L.ttab[(size_t)solve * L.nev + e] = (float)u[brick_index<R>(L, x, y, z)];
-            }
+            for (int e = lane; e < L.nev; e += 64) L.ttab[(size_t)solve * L.nev + e] = event_time<R>(L, u, e);
         }
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

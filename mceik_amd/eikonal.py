@@ -219,8 +219,12 @@ class BatchSolver:
         return b
 
     def solve(self, sources, slow, ev_node=None, want_fields=False, max_sweeps=-1, stream=None,
-              solve_order=None, solve_clock=False, max_waves=0, step_z=0):
-        """solve_order: optional permutation of the nmodel*nstat solve ids (the
+              solve_order=None, solve_clock=False, max_waves=0, step_z=0, ev_frac=None):
+        """ev_node: [nev] x-fastest node per event -> out["ttab"] [nsolve][nev]
+        (fp32): the node's value, or with ev_frac ([nev][3] float32 fractions,
+        ev_node = the lowest corner of the event's cell; `cell_corners`) the
+        trilinear interpolation in that cell (mceik_fsm_batch.ev_frac).
+        solve_order: optional permutation of the nmodel*nstat solve ids (the
         order the work queues hand them out; results do not depend on it).
         solve_clock: also return out["clock"] [nsolve][2], the device realtime
         (100 MHz) at the start and end of every solve.  max_waves: cap on the
@@ -267,6 +271,12 @@ class BatchSolver:
             b.ev_node, b.ttab = ev_node.data_ptr(), ttab.data_ptr()
             out["ttab"] = ttab
             out["_ev"] = ev_node
+            if ev_frac is not None:
+                ev_frac = torch.as_tensor(ev_frac, dtype=torch.float32).to(dev).contiguous()
+                if ev_frac.numel() != 3 * nev:
+                    raise ValueError("ev_frac must hold 3 fractions per event")
+                b.ev_frac = ev_frac.data_ptr()
+                out["_evf"] = ev_frac
         if want_fields:
             u = torch.empty((nsolve, self.nz, self.ny, self.nx), dtype=want_dtype, device=dev)
             b.u_out = u.data_ptr()

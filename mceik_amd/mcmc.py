@@ -58,6 +58,7 @@ class Problem:
     nburn: int = 0
     keepk: int = 1
     niter: int = 0                  # mcparms.niter: total proposals (Sampler.run(-1) runs the rest)
+    tt_interp: int = 0              # 0: event times at the nearest node (reference); 1: trilinear in the cell
     v_true: np.ndarray = None       # [ncell] int, model used to make the picks
     _keep: list = field(default_factory=list, repr=False)
 
@@ -108,6 +109,23 @@ class Problem:
             return i
         ix, iy, iz = idx(self.nx, self.x0, self.ex), idx(self.ny, self.y0, self.ey), idx(self.nz, self.z0, self.ez)
         return ((iz * self.ny + iy) * self.nx + ix).astype(np.int32)
+
+    @property
+    def ev_cell(self):
+        """Trilinear mode (tt_interp = 1): (lowest corner node [nev] int32, fractions
+        [nev][3] float32) of each event's grid cell, as mceik_mcmc_init computes them
+        (capi.hip cell_corner: i = trunc((x - x0)/h) clamped to [0, n-2], w = f - i in
+        [0, 1] rounded once to fp32)."""
+        def corner(n, x0, xs):
+            f = (np.asarray(xs, dtype=np.float64) - x0) / self.h
+            i = np.where(f <= 0.0, 0, np.trunc(np.maximum(f, 0.0))).astype(np.int64)
+            i = np.minimum(i, n - 2)
+            w = np.clip(f - i, 0.0, 1.0).astype(np.float32)
+            return i, w
+        ix, wx = corner(self.nx, self.x0, self.ex)
+        iy, wy = corner(self.ny, self.y0, self.ey)
+        iz, wz = corner(self.nz, self.z0, self.ez)
+        return ((iz * self.ny + iy) * self.nx + ix).astype(np.int32), np.stack([wx, wy, wz], 1)
 
     @property
     def obs_mask(self):
@@ -250,6 +268,7 @@ class Sampler:
         o.vmin, o.vmax, o.dvmax, o.seed = p.vmin, p.vmax, p.dvmax, p.seed
         o.max_samples, o.device = int(max_samples), int(device)
         o.precision, o.max_waves = int(precision), int(max_waves)
+        o.tt_interp = int(p.tt_interp)
         h = C.c_void_p()
         rc = L.mceik_mcmc_init(C.byref(parms), C.byref(st), C.byref(cat), C.byref(o),
                                self.v0.ctypes.data_as(C.c_void_p), C.byref(h))

@@ -292,7 +292,33 @@ typedef struct {
     const double *tobs, *tcorr, *var;
     int vmin, vmax, dvmax;
     uint32_t seed;
+    const float *ev_frac;         /* NULL, or trilinear mode: [nevents][3] fractions, ev_node = cell corner */
 } oracle_mcmc_problem;
+
+/* Travel time of an event from a solved fp32 field u (x fastest).  w == NULL:
+ * the node value (the reference's nearest-node snapping, fsm3d.f90:697-711).
+ * Else the build's trilinear mode (no reference counterpart, parity unpinned
+ * by the reference): corners clamped to the grid, x then y then z, each lerp
+ * a + w*(b - a) in fp32 (this file is compiled without contraction), the
+ * GPU's event_time (mceik_amd/csrc/fsm_device.h) operation for operation. */
+float oracle_event_time(const float *u, int nx, int ny, int nz, int node, const float *w)
+{
+    if (!w) return u[node];
+    int nxy = nx * ny, z = node / nxy, y = (node - z * nxy) / nx, x = node - z * nxy - y * nx;
+    int x1 = x + 1 < nx ? x + 1 : nx - 1, y1 = y + 1 < ny ? y + 1 : ny - 1, z1 = z + 1 < nz ? z + 1 : nz - 1;
+    float c[8], a[4];
+    for (int k = 0; k < 8; k++)
+        c[k] = u[(size_t)((k & 4) ? z1 : z) * nxy + (size_t)((k & 2) ? y1 : y) * nx + ((k & 1) ? x1 : x)];
+    for (int k = 0; k < 4; k++) {
+        float d = c[2 * k + 1] - c[2 * k];
+        float m = w[0] * d;
+        a[k] = c[2 * k] + m;
+    }
+    float d0 = a[1] - a[0], m0 = w[1] * d0, b0 = a[0] + m0;
+    float d1 = a[3] - a[2], m1 = w[1] * d1, b1 = a[2] + m1;
+    float d2 = b1 - b0, m2 = w[2] * d2;
+    return b0 + m2;
+}
 
 void oracle_expand_slowness(const oracle_mcmc_problem *p, const int *v, float *slow)
 {
@@ -322,7 +348,9 @@ int oracle_forward_f32(const oracle_mcmc_problem *p, const int *v, float *ttab, 
                                            p->x0, p->y0, p->z0, &ts, &p->sx[s], &p->sy[s],
                                            &p->sz[s], slow, u, &it) != 0;
         if (niter) niter[s] = it;
-        for (int e = 0; e < p->nevents; e++) ttab[(size_t)s * p->nevents + e] = u[p->ev_node[e]];
+        for (int e = 0; e < p->nevents; e++)
+            ttab[(size_t)s * p->nevents + e] = oracle_event_time(u, p->nx, p->ny, p->nz, p->ev_node[e],
+                                                                 p->ev_frac ? p->ev_frac + 3 * e : NULL);
         free(u);
     }
     free(slow);

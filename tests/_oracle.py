@@ -110,7 +110,8 @@ class McmcProblem(C.Structure):
                [("nstat", C.c_int), ("nevents", C.c_int)] + \
                [(n, C.c_void_p) for n in ("sx", "sy", "sz", "ev_node", "obs_ptr", "obs_stat", "obs_mask",
                                           "tobs", "tcorr", "var")] + \
-               [("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int), ("seed", C.c_uint32)]
+               [("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int), ("seed", C.c_uint32),
+                ("ev_frac", C.c_void_p)]
 
 
 def make_problem(pb):
@@ -123,12 +124,19 @@ def make_problem(pb):
         setattr(P, n, float(getattr(pb, n)))
     P.seed = int(pb.seed)
     keep = []
+    interp = bool(getattr(pb, "tt_interp", 0))
+    ev_node, ev_frac = pb.ev_cell if interp else (pb.ev_node, None)
+    vals = {"ev_node": ev_node}
     for n, dt in (("sx", np.float64), ("sy", np.float64), ("sz", np.float64), ("ev_node", np.int32),
                   ("obs_ptr", np.int32), ("obs_stat", np.int32), ("obs_mask", np.int32),
                   ("tobs", np.float64), ("tcorr", np.float64), ("var", np.float64)):
-        a = np.ascontiguousarray(getattr(pb, n), dtype=dt)
+        a = np.ascontiguousarray(vals[n] if n in vals else getattr(pb, n), dtype=dt)
         keep.append(a)
         setattr(P, n, a.ctypes.data)
+    if interp:
+        a = np.ascontiguousarray(ev_frac, dtype=np.float32)
+        keep.append(a)
+        P.ev_frac = a.ctypes.data
     P._keep = keep
     return P
 
@@ -139,6 +147,16 @@ def forward_f32(P, v):
     v = np.ascontiguousarray(v, dtype=np.int32)
     lib().oracle_forward_f32(C.byref(P), _p(v), _p(tt), _p(it))
     return tt.reshape(P.nstat, P.nevents), it
+
+
+def event_time(u, nx, ny, nz, node, w=None):
+    """oracle_event_time: node value (w None) or the trilinear fp32 value."""
+    L = lib()
+    L.oracle_event_time.restype = C.c_float
+    L.oracle_event_time.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    u = np.ascontiguousarray(u, dtype=np.float32)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float32)
+    return np.float32(L.oracle_event_time(_p(u), nx, ny, nz, int(node), _p(w)))
 
 
 def loglik(P, tt):

@@ -66,3 +66,37 @@ def test_oracle_mcmc_accept_rejects_outside_prior():
     tt, _ = O.forward_f32(P, v[0])
     vo, lo, acc, _ = O.mcmc_run(P, v, [O.loglik(P, tt)], 0, 0, 5)
     assert acc.sum() <= 5 and np.all((vo >= 3000) & (vo <= 3001))
+
+
+def test_trilinear_event_time_restatement():
+    """oracle_event_time (the trilinear mode's checker): exact on a linear field
+    with dyadic fractions, the node value at w = 0 or w = None, corner clamping
+    on the grid's last plane."""
+    nx, ny, nz = 5, 4, 3
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    u = (1.0 + 2.0 * i + 4.0 * j + 8.0 * k).astype(np.float32).ravel()
+    rng = np.random.default_rng(2)
+    for _ in range(50):
+        x, y, z = rng.integers(0, nx - 1), rng.integers(0, ny - 1), rng.integers(0, nz - 1)
+        w = rng.integers(0, 5, 3) / 4.0
+        node = (z * ny + y) * nx + x
+        t = O.event_time(u, nx, ny, nz, node, w)
+        assert t == np.float32(1.0 + 2.0 * (x + w[0]) + 4.0 * (y + w[1]) + 8.0 * (z + w[2]))
+        assert O.event_time(u, nx, ny, nz, node, np.zeros(3)) == u[node] == O.event_time(u, nx, ny, nz, node)
+    last = (nz - 1) * nx * ny + (ny - 1) * nx + nx - 1      # corners clamp to the grid
+    assert O.event_time(u, nx, ny, nz, last, np.full(3, 0.5)) == u[last]
+
+
+def test_event_cells_trilinear_mode():
+    """Problem.ev_cell: lowest corner clamped to [0, n-2], fractions in [0, 1];
+    on-node events get fraction 0 (or 1 on the last plane)."""
+    p = mcmc.Problem(nx=10, ny=8, nz=6, h=100.0, x0=50.0)
+    p.ex = np.array([50.0, 150.0, 925.0, -10.0, 2000.0, 925.0 - 1e-9])
+    p.ey = np.array([0.0, 100.0, 700.0, 0.0, 0.0, 350.0])
+    p.ez = np.array([0.0, 500.0, 250.0, -5.0, 0.0, 0.0])
+    node, w = p.ev_cell
+    ix, iy, iz = node % 10, (node // 10) % 8, node // 80
+    assert list(ix) == [0, 1, 8, 0, 8, 8] and list(iy) == [0, 1, 6, 0, 0, 3] and list(iz) == [0, 4, 2, 0, 0, 0]
+    assert w.dtype == np.float32 and np.all((w >= 0) & (w <= 1))
+    assert list(w[:, 0]) == [0.0, 0.0, np.float32(0.75), 0.0, 1.0, np.float32(0.75 - 1e-11)]
+    assert w[1, 2] == 1.0 and w[2, 1] == 1.0 and w[5, 1] == 0.5
