@@ -37,6 +37,26 @@ typedef struct mceik_mcmc_opts {
                                   interpolation in the event's grid cell (mceik_fsm_batch.ev_frac) */
 } mceik_mcmc_opts;
 
+/* ---- run configuration (host only; csrc/parms.c) ----------------------
+ * The reference's mains hard-code their parameters (homog.c:73-89,
+ * fsm3d.f90:2085-2100); these fill mceik_parms_struct (mceik_struct.h:68-90)
+ * and the sampler options from an INI file ([general] projnm scratch_dir;
+ * [grid] x0 y0 z0 dx dy dz nx ny nz ndivx ndivy ndivz nrefx nrefy nrefz
+ * tt_interp; [eikonal] tol maxit precision max_waves; [mcmc] resdir nburnIn
+ * niter keepK nchains chain_offset vmin vmax dvmax seed max_samples device),
+ * names case-insensitive, ';'/'#' comments.  Either record pointer may be NULL. */
+/* homog.c's grid (32 x 29 x 26 nodes at 1 km), tol 1e-8, maxit 50, seed 2016. */
+int mceik_parms_defaults(struct mceik_parms_struct *parms, mceik_mcmc_opts *opts);
+/* key "section:name": 0 ok, 1 unknown key, 2 invalid value (message on stderr). */
+int mceik_parms_set(struct mceik_parms_struct *parms, mceik_mcmc_opts *opts, const char *key, const char *value);
+/* 0 ok, -1 cannot open, > 0 the line number of the first bad line. */
+int mceik_parms_read(const char *path, struct mceik_parms_struct *parms, mceik_mcmc_opts *opts);
+/* Applies [--]section:key=value arguments and --config FILE / --config=FILE
+ * (in argument order, argv[0] skipped); returns the count consumed or -1. */
+int mceik_parms_args(int argc, char **argv, struct mceik_parms_struct *parms, mceik_mcmc_opts *opts);
+/* Writes every key back in INI form (0 ok). */
+int mceik_parms_write(const char *path, const struct mceik_parms_struct *parms, const mceik_mcmc_opts *opts);
+
 /* v0: host [nchains][ncell] int m/s, ncell = ceil(nx/nrefx)*ceil(ny/nrefy)*
  * ceil(nz/nrefz), cell index x fastest.  Computes each chain's initial logL. */
 int mceik_mcmc_init(const struct mceik_parms_struct *parms,

@@ -86,7 +86,8 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_i
            "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
-           "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize")
+           "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize",
+           "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write")
 
 
 def lib():
