@@ -170,6 +170,16 @@ def main():
     stream = torch.cuda.current_stream(dev)
     smp.set_stream(stream.cuda_stream)
 
+    comm = post = None
+    if world > 1:
+        # the library's checkpoint gather (mceik_mcmc_gather, RCCL over xGMI);
+        # the id travels over the torch.distributed group, as MPI_Bcast would carry it
+        comm = mcmc.Comm.from_torch(local_rank)
+        if rank == 0:
+            post = torch.empty((per_gpu * world, p.ncell), dtype=torch.int32, device=dev)
+            post_l = torch.empty(per_gpu * world, dtype=torch.float64, device=dev)
+    else:
+        post = torch.empty((hi - lo, p.ncell), dtype=torch.int32, device=dev)
     if args.warmup:
         smp.run(args.warmup)
     smp.fsm_stats(reset=True)
@@ -181,9 +191,8 @@ def main():
     smp.run(args.steps)
     # checkpoint: the kept posterior states of every chain -> rank 0 (RCCL over xGMI)
     if world > 1:
-        post, _ = mcmc.gather_kept(smp, per_gpu * world, device=dev)
+        comm.gather(smp, per_gpu * world, which=1, root=0, v_out=post, logl_out=post_l if rank == 0 else None)
     else:
-        post = torch.empty((hi - lo, p.ncell), dtype=torch.int32, device=dev)
         smp.samples(max_states=1, device_ptr=post.data_ptr())
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -194,6 +203,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    gather_check = None
+    if world > 1:
+        # outside the timed region: the library gather == torch.distributed's gather
+        tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=dev)
+        if rank == 0:
+            gather_check = bool(torch.equal(tv, post) and torch.equal(tl, post_l))
+        comm.close()
     fsm_ms, nlaunch, iters, (bricks, segs, segs_changed) = smp.fsm_stats()
     _, logl, nacc, _ = smp.state()
     smp.close()
@@ -258,6 +274,8 @@ def main():
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
+        if gather_check is not None:
+            line["gather"] = {"path": "mceik_mcmc_gather (RCCL)", "equals_torch_gather": gather_check}
         if args.raw_stats:
             line["fsm_raw"] = {"bricks": bricks, "segs": segs, "segs_changed": segs_changed, "iters": iters,
                                "launches": nlaunch}

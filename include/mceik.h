@@ -99,6 +99,30 @@ int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsi
                          unsigned long long *visits, int reset);
 int mceik_mcmc_finalize(mceik_mcmc **s);
 
+/* ---- multi-rank runs (one process per GPU; csrc/comm.hip) ---------------
+ * The sampler's only collective is the checkpoint gather (SURVEY s.8e) over
+ * RCCL (xGMI on one node).  Bootstrap as RCCL's: rank 0 calls
+ * mceik_comm_unique_id, the launcher broadcasts the bytes (MPI_Bcast in a
+ * C/MPI main -- MPI keeps launch and bootstrap, the role of broadcast.c and
+ * mpiutils.f90:346-426), then every rank calls mceik_comm_init with its GPU. */
+#define MCEIK_COMM_ID_BYTES 128
+typedef struct mceik_comm mceik_comm;
+int mceik_comm_unique_id(unsigned char id[MCEIK_COMM_ID_BYTES]);
+int mceik_comm_init(const unsigned char id[MCEIK_COMM_ID_BYTES], int nranks, int rank, int device,
+                    mceik_comm **out);
+int mceik_comm_finalize(mceik_comm **c);
+/* Collective over c: every rank's chains -> root, in global chain order.
+ * which = 0 the current state (mceik_mcmc_get_state), 1 the most recent kept
+ * state (every rank must hold one).  The ranks' shards [chain_offset,
+ * chain_offset + nchains) must tile [0, nchains_total) (else every rank
+ * returns 2).  On the root v_out [nchains_total][ncell] and logl_out
+ * [nchains_total] are host or device memory (either may be NULL; device
+ * memory of the communicator's GPU is received into directly, without
+ * staging); other ranks pass NULL.
+ * Synchronises the sampler's stream. */
+int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nchains_total, int root, int *v_out,
+                      double *logl_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,7 +87,8 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_i
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
            "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize",
-           "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write")
+           "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write",
+           "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather")
 
 
 def lib():
@@ -152,6 +153,14 @@ def lib():
     L.mceik_mcmc_fsm_stats.restype = C.c_int
     L.mceik_mcmc_fsm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong),
                                        C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]
+    L.mceik_comm_unique_id.restype = C.c_int
+    L.mceik_comm_unique_id.argtypes = [C.c_void_p]
+    L.mceik_comm_init.restype = C.c_int
+    L.mceik_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.mceik_comm_finalize.restype = C.c_int
+    L.mceik_comm_finalize.argtypes = [C.POINTER(C.c_void_p)]
+    L.mceik_mcmc_gather.restype = C.c_int
+    L.mceik_mcmc_gather.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
     L.mceik_mcmc_finalize.restype = C.c_int
     L.mceik_mcmc_finalize.argtypes = [C.POINTER(C.c_void_p)]
     _lib = L

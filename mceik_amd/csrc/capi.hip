@@ -1253,6 +1253,25 @@ extern "C" int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_o
     return 0;
 }
 
+// Device view of this sampler's chain shard for comm.hip's gather: which = 0
+// the current state, 1 the most recent kept state (1 if none is kept).
+int mcmc_shard_view(mceik_mcmc *s, int which, McmcShard *out)
+{
+    if (!s || !out) return 1;
+    const McmcDev &D = s->D;
+    out->device = s->device; out->stream = s->stream;
+    out->nchains = D.nchains; out->chain_offset = D.chain_offset; out->ncell = D.ncell;
+    if (which == 0) {
+        out->v = D.v; out->logl = D.logl;
+        return 0;
+    }
+    if (s->max_samples <= 0 || s->nkept - s->nkept_base <= 0) return 1;
+    const int slot = (int)(((long long)s->nkept - 1) % s->max_samples);
+    out->v = D.keep_v + (size_t)slot * D.nchains * D.ncell;
+    out->logl = D.keep_logl + (size_t)slot * D.nchains;
+    return 0;
+}
+
 extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept,
                                const int **ierr)
 {

@@ -1,0 +1,252 @@
+// comm.hip -- multi-rank runs from C (include/mceik.h mceik_comm_*,
+// mceik_mcmc_gather): the sampler's only collective, the checkpoint gather of
+// every rank's chain shard to a root rank over RCCL (xGMI on one node;
+// SURVEY s.8e).
+//
+// The reference's multi-rank flow is MPI end to end: broadcast.c:14-143 sends
+// the catalogue/stations from the master, mpiutils.f90:346-426 splits the
+// communicators, homog.c:343-415 has rank 0 gather and write.  Here a C/MPI
+// main keeps MPI for launch and bootstrap only (one rank per GPU): rank 0
+// makes the RCCL id, the main broadcasts its 128 bytes (MPI_Bcast), every
+// rank builds the communicator and calls mceik_mcmc_gather at a checkpoint.
+//
+// RCCL is opened on first use (dlopen "librccl.so.1", the same library torch's
+// nccl backend loads), so the product library carries no link dependency on
+// it and single-GPU callers never load it.
+#include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/mceik.h"
+#include "mcmc_common.h"
+
+namespace {
+
+struct Rccl {
+    bool ok = false;
+    const char *(*GetErrorString)(ncclResult_t);
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *);
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
+    ncclResult_t (*CommDestroy)(ncclComm_t);
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*GroupStart)();
+    ncclResult_t (*GroupEnd)();
+};
+
+const Rccl &rccl()
+{
+    static Rccl r = [] {
+        Rccl x;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            fprintf(stderr, "mceik_comm: cannot load RCCL (%s)\n", dlerror());
+            return x;
+        }
+        bool all = true;
+        auto get = [&](auto &fn, const char *name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn) { fprintf(stderr, "mceik_comm: RCCL lacks %s\n", name); all = false; }
+        };
+        get(x.GetErrorString, "ncclGetErrorString");
+        get(x.GetUniqueId, "ncclGetUniqueId");
+        get(x.CommInitRank, "ncclCommInitRank");
+        get(x.CommDestroy, "ncclCommDestroy");
+        get(x.AllGather, "ncclAllGather");
+        get(x.Send, "ncclSend");
+        get(x.Recv, "ncclRecv");
+        get(x.GroupStart, "ncclGroupStart");
+        get(x.GroupEnd, "ncclGroupEnd");
+        x.ok = all;
+        return x;
+    }();
+    return r;
+}
+
+}  // namespace
+
+// Runs the calling scope on `dev` and restores the caller's device.
+struct DevScope {
+    int prev = -1;
+    explicit DevScope(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DevScope()
+    {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
+// true if p is device memory of GPU `dev` (the gather then receives into it)
+static bool on_device(const void *p, int dev)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice && a.device == dev;
+}
+
+struct mceik_comm {
+    ncclComm_t comm;
+    int nranks, rank, device;
+    int *d_shard;          // [nranks][2] (chain_offset, nchains) exchange buffer
+};
+
+#define RCCLCHK(x)                                                                         \
+    do {                                                                                   \
+        ncclResult_t r_ = (x);                                                             \
+        if (r_ != ncclSuccess) {                                                           \
+            fprintf(stderr, "mceik_comm: %s failed: %s\n", #x, rccl().GetErrorString(r_)); \
+            return -1;                                                                     \
+        }                                                                                  \
+    } while (0)
+#define HIPCHK2(x)                                                                         \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "mceik_comm: %s failed: %s\n", #x, hipGetErrorString(e_));     \
+            return -1;                                                                     \
+        }                                                                                  \
+    } while (0)
+
+extern "C" int mceik_comm_unique_id(unsigned char id[MCEIK_COMM_ID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) == MCEIK_COMM_ID_BYTES, "RCCL id size");
+    if (!id || !rccl().ok) return 1;
+    ncclUniqueId u;
+    RCCLCHK(rccl().GetUniqueId(&u));
+    memcpy(id, &u, sizeof(u));
+    return 0;
+}
+
+extern "C" int mceik_comm_init(const unsigned char id[MCEIK_COMM_ID_BYTES], int nranks, int rank, int device,
+                               mceik_comm **out)
+{
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || !rccl().ok) return 1;
+    *out = nullptr;
+    DevScope dg(device);
+    mceik_comm *c = new mceik_comm();
+    c->nranks = nranks; c->rank = rank; c->device = device;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, u, rank);
+    hipError_t e = r == ncclSuccess ? hipMalloc(&c->d_shard, (size_t)nranks * 2 * sizeof(int)) : hipSuccess;
+    if (r != ncclSuccess || e != hipSuccess) {
+        fprintf(stderr, "mceik_comm_init: %s\n", r != ncclSuccess ? rccl().GetErrorString(r) : hipGetErrorString(e));
+        if (r == ncclSuccess) rccl().CommDestroy(c->comm);
+        delete c;
+        return -1;
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" int mceik_comm_finalize(mceik_comm **pc)
+{
+    if (!pc || !*pc) return 0;
+    mceik_comm *c = *pc;
+    ncclResult_t r;
+    {
+        DevScope dg(c->device);
+        hipFree(c->d_shard);
+        r = rccl().CommDestroy(c->comm);
+    }
+    delete c;
+    *pc = nullptr;
+    return r == ncclSuccess ? 0 : -1;
+}
+
+// Collective.  Every rank's shard [chain_offset, chain_offset + nchains) is
+// sent to `root`, which receives it at its global position: point-to-point
+// send/recv in one RCCL group (shards may differ in size, no padding), the
+// root's own shard by a device copy.  The shards must tile [0, nchains_total)
+// (every rank checks the all-gathered (offset, count) table, so all return alike).
+extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nchains_total, int root,
+                                 int *v_out, double *logl_out)
+{
+    if (!s || !c || root < 0 || root >= c->nranks || nchains_total < 1) return 1;
+    McmcShard sh;
+    int have = mcmc_shard_view(s, which, &sh) == 0;
+    if (sh.device != c->device) {
+        fprintf(stderr, "mceik_mcmc_gather: sampler on device %d, communicator on %d\n", sh.device, c->device);
+        return 1;
+    }
+    DevScope dg(c->device);
+    hipStream_t st = (hipStream_t)sh.stream;
+    // 1. every rank learns every shard (a rank without a kept state sends count -1)
+    const int mine[2] = {sh.chain_offset, have ? sh.nchains : -1};
+    std::vector<int> all((size_t)c->nranks * 2);
+    int rc = 0;
+    HIPCHK2(hipMemcpyAsync(c->d_shard + 2 * c->rank, mine, sizeof(mine), hipMemcpyHostToDevice, st));
+    RCCLCHK(rccl().AllGather(c->d_shard + 2 * c->rank, c->d_shard, 2, ncclInt32, c->comm, st));
+    HIPCHK2(hipMemcpyAsync(all.data(), c->d_shard, all.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK2(hipStreamSynchronize(st));
+    {   // the shards must tile [0, nchains_total): every rank checks the same table
+        std::vector<int> cover((size_t)nchains_total, 0);
+        for (int r = 0; r < c->nranks && !rc; r++) {
+            const int off = all[2 * r], n = all[2 * r + 1];
+            if (n < 0 || off < 0 || (long long)off + n > nchains_total) { rc = 2; break; }
+            for (int k = off; k < off + n; k++) cover[k]++;
+        }
+        for (int k = 0; k < nchains_total && !rc; k++) if (cover[k] != 1) rc = 2;
+        if (rc) {
+            if (c->rank == root)
+                fprintf(stderr, "mceik_mcmc_gather: the ranks' shards (or kept states) do not tile [0, %d)\n",
+                        nchains_total);
+            return rc;
+        }
+    }
+    const size_t ncell = (size_t)sh.ncell;
+    // root: receive straight into caller device memory on this GPU, else into a staging buffer
+    int *d_v = nullptr;
+    double *d_l = nullptr;
+    bool stage_v = false, stage_l = false;
+    if (c->rank == root) {
+        stage_v = !on_device(v_out, c->device);
+        stage_l = !on_device(logl_out, c->device);
+        if (stage_v) HIPCHK2(hipMallocAsync((void **)&d_v, (size_t)nchains_total * ncell * sizeof(int), st));
+        else d_v = v_out;
+        if (stage_l) HIPCHK2(hipMallocAsync((void **)&d_l, (size_t)nchains_total * sizeof(double), st));
+        else d_l = logl_out;
+    }
+    // 2. shards to the root
+    RCCLCHK(rccl().GroupStart());
+    if (c->rank == root) {
+        for (int r = 0; r < c->nranks; r++) {
+            if (r == root) continue;
+            const size_t off = (size_t)all[2 * r], n = (size_t)all[2 * r + 1];
+            RCCLCHK(rccl().Recv(d_v + off * ncell, n * ncell, ncclInt32, r, c->comm, st));
+            RCCLCHK(rccl().Recv(d_l + off, n, ncclFloat64, r, c->comm, st));
+        }
+    } else {
+        RCCLCHK(rccl().Send(sh.v, (size_t)sh.nchains * ncell, ncclInt32, root, c->comm, st));
+        RCCLCHK(rccl().Send(sh.logl, (size_t)sh.nchains, ncclFloat64, root, c->comm, st));
+    }
+    RCCLCHK(rccl().GroupEnd());
+    if (c->rank == root) {
+        const size_t off = (size_t)sh.chain_offset;
+        HIPCHK2(hipMemcpyAsync(d_v + off * ncell, sh.v, (size_t)sh.nchains * ncell * sizeof(int),
+                               hipMemcpyDeviceToDevice, st));
+        HIPCHK2(hipMemcpyAsync(d_l + off, sh.logl, (size_t)sh.nchains * sizeof(double), hipMemcpyDeviceToDevice, st));
+        if (stage_v && v_out)
+            HIPCHK2(hipMemcpyAsync(v_out, d_v, (size_t)nchains_total * ncell * sizeof(int), hipMemcpyDefault, st));
+        if (stage_l && logl_out)
+            HIPCHK2(hipMemcpyAsync(logl_out, d_l, (size_t)nchains_total * sizeof(double), hipMemcpyDefault, st));
+        if (stage_v) HIPCHK2(hipFreeAsync(d_v, st));
+        if (stage_l) HIPCHK2(hipFreeAsync(d_l, st));
+    }
+    HIPCHK2(hipStreamSynchronize(st));
+    return 0;
+}

@@ -20,3 +20,14 @@ struct McmcDev {
     int *keep_v;                   // [max_samples][nchains][ncell]
     double *keep_logl;             // [max_samples][nchains]
 };
+
+// One rank's chain shard as the checkpoint gather sees it (capi.hip
+// mcmc_shard_view -> comm.hip).  stream is a hipStream_t.
+struct mceik_mcmc;
+struct McmcShard {
+    int device, nchains, chain_offset, ncell;
+    void *stream;
+    const int *v;                  // device [nchains][ncell]
+    const double *logl;            // device [nchains]
+};
+int mcmc_shard_view(mceik_mcmc *s, int which, McmcShard *out);

@@ -434,3 +434,67 @@ def gather_kept(smp: Sampler, nchains_total, group=None, dst=0, device=None):
     parts = [shard(nchains_total, r, world) for r in range(world)]
     return (torch.cat([gv[r][:hi - lo] for r, (lo, hi) in enumerate(parts)]),
             torch.cat([gl[r][:hi - lo] for r, (lo, hi) in enumerate(parts)]))
+
+
+class Comm:
+    """RCCL communicator of the library's checkpoint gather (include/mceik.h
+    mceik_comm_*): one rank per GPU.  `bootstrap` moves the 128-byte id from
+    rank 0 to the others (an MPI main uses MPI_Bcast; here any callable
+    bytes -> bytes, e.g. over torch.distributed: see `from_torch`)."""
+
+    def __init__(self, rank, world, device, bootstrap=None):
+        L = _lib.lib()
+        uid = (C.c_ubyte * 128)()
+        if rank == 0 and L.mceik_comm_unique_id(uid) != 0:
+            raise RuntimeError("mceik_comm_unique_id failed")
+        if world > 1:
+            got = bootstrap(bytes(uid) if rank == 0 else None)
+            C.memmove(uid, got, 128)
+        h = C.c_void_p()
+        if L.mceik_comm_init(uid, int(world), int(rank), int(device), C.byref(h)) != 0:
+            raise RuntimeError("mceik_comm_init failed")
+        self._h, self._L, self.rank, self.world = h, L, rank, world
+
+    @classmethod
+    def from_torch(cls, device, group=None):
+        """Bootstrap over an initialised torch.distributed group."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+        def bcast(b):
+            box = [b]
+            dist.broadcast_object_list(box, src=0, group=group)
+            return box[0]
+        return cls(rank, world, device, bcast)
+
+    def gather(self, smp: Sampler, nchains_total, which=1, root=0, v_out=None, logl_out=None):
+        """mceik_mcmc_gather: every rank's chains -> `root` in global chain order.
+        which 0 = current state, 1 = most recent kept state.  v_out / logl_out:
+        torch tensors (device: received in place) or numpy arrays on the root;
+        by default the root gets host numpy arrays.  Returns (v, logl) on the
+        root, (None, None) elsewhere."""
+        is_root = self.rank == root
+        if is_root and v_out is None:
+            v_out = np.empty((nchains_total, smp.p.ncell), np.int32)
+            logl_out = np.empty(nchains_total, np.float64) if logl_out is None else logl_out
+
+        def ptr(a):
+            if a is None or not is_root:
+                return None
+            return a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data
+        rc = self._L.mceik_mcmc_gather(smp._h, self._h, int(which), int(nchains_total), int(root),
+                                       ptr(v_out), ptr(logl_out))
+        if rc != 0:
+            raise RuntimeError(f"mceik_mcmc_gather failed ({rc})")
+        return (v_out, logl_out) if is_root else (None, None)
+
+    def close(self):
+        if self._h:
+            self._L.mceik_comm_finalize(C.byref(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -74,3 +74,35 @@ def test_two_rank_samplers_gather_equals_single_process():
     s.close()
     assert got_v.shape == (NCHAINS, v.shape[2])
     assert np.array_equal(got_v, v[0]) and np.array_equal(got_l.view(np.uint64), lg[0].view(np.uint64))
+
+
+def test_library_rccl_gather_single_rank():
+    """mceik_comm_* / mceik_mcmc_gather (the C multi-rank path, RCCL) with one
+    rank: kept and current states land in global chain order, into host arrays
+    or straight into a device tensor; shards that do not tile the chain range
+    and a missing kept state are refused.  (More ranks need more GPUs: RCCL
+    takes one rank per device; the driver's 8-GPU bench runs that path.)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mceik_amd import mcmc
+    comm = mcmc.Comm(0, 1, 0)
+    s = mcmc.Sampler(_problem(), nchains=NCHAINS, max_samples=2)
+    s.run(NSTEPS)
+    kv, kl = s.samples(max_states=1)
+    v, lg, _, _ = s.state()
+    gv, gl = comm.gather(s, NCHAINS, which=1)
+    assert np.array_equal(gv, kv[0]) and np.array_equal(gl.view(np.uint64), kl[0].view(np.uint64))
+    cv, cl = comm.gather(s, NCHAINS, which=0)
+    assert np.array_equal(cv, v) and np.array_equal(cl.view(np.uint64), lg.view(np.uint64))
+    dv = torch.zeros((NCHAINS, s.p.ncell), dtype=torch.int32, device="cuda:0")
+    dl = torch.zeros(NCHAINS, dtype=torch.float64, device="cuda:0")
+    comm.gather(s, NCHAINS, which=1, v_out=dv, logl_out=dl)
+    assert np.array_equal(dv.cpu().numpy(), kv[0]) and np.array_equal(dl.cpu().numpy(), kl[0])
+    with pytest.raises(RuntimeError):
+        comm.gather(s, NCHAINS + 1)                       # chain NCHAINS is on no rank
+    s.close()
+    s0 = mcmc.Sampler(_problem(), nchains=NCHAINS, max_samples=0)
+    with pytest.raises(RuntimeError):
+        comm.gather(s0, NCHAINS, which=1)                 # nothing kept
+    s0.close()
+    comm.close()

@@ -126,3 +126,26 @@ def test_locate3d_gridsearch_bitwise_vs_reference(prec):
     assert locate3d_gridsearch(ld, ld + 64, no, 1, g["mask"], g["tobs"], g["varobs"], big, lp) == g[f"ierr{prec}_ng"] == 1
     assert locate3d_gridsearch(ld, ng, no, 1, np.ones(no), g["tobs"], g["varobs"], g["test"], lp[:ng]) == \
         g[f"ierr{prec}_allmasked"] == 1
+
+
+def test_c_sampler_main_config_checkpoint_gather(tmp_path):
+    """tests/c/mcmc_main.c: a C main using only include/mceik.h -- INI config +
+    argv overrides, sampler run to mcparms.niter, checkpoint -> restore in a
+    second sampler continuing bitwise, and the RCCL checkpoint gather."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = str(tmp_path / "mcmc_main")
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c", "mcmc_main.c"),
+                    "-L", os.path.join(ROOT, "mceik_amd"), "-lmceik_hip", "-Wl,-rpath," + os.path.join(ROOT, "mceik_amd"),
+                    "-lm", "-o", exe], check=True)
+    ini = tmp_path / "run.ini"
+    ini.write_text("[grid]\nnx = 24\nny = 20\nnz = 28\ndx = 100\ndy = 100\ndz = 100\n"
+                   "nrefx = 4\nnrefy = 4\nnrefz = 4\n[eikonal]\ntol = 1e-8\nmaxit = 30\n"
+                   "[mcmc]\nnchains = 6\nniter = 8\nnburnIn = 2\nkeepK = 1\nmax_samples = 2\n"
+                   "dvmax = 300\nvmin = 2000\nvmax = 7000\n")
+    out = subprocess.run([exe, "--config", str(ini), "mcmc:seed=77"], capture_output=True, text=True, timeout=120)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    checks = {ln.split()[1]: ln.split()[2] for ln in out.stdout.splitlines() if ln.startswith("check ")}
+    assert len(checks) == 6 and all(v == "1" for v in checks.values()), checks
+    assert "chains 6 step 8" in out.stdout
