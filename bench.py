@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v25"          # bump when the sweep kernel changes; profiles/traffic.json must match
+KERNEL_REV = "fsm-v26"          # bump when the sweep kernel changes; profiles/traffic.json must match
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--cpu-rounds", type=int, default=CPU_ROUNDS)
     ap.add_argument("--sigma", type=float, default=5e-4, help="pick noise (s); varObs = sigma^2")
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
+    ap.add_argument("--precision", type=int, default=32, choices=(32, 64),
+                    help="FSM arithmetic (64: the reference's literal fp64 update; tables fp32 either way)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -166,7 +168,8 @@ def main():
     p.tobs = tt.T.ravel().astype(np.float64) + rng.normal(0.0, args.sigma, p.nevents * p.nstat)
     p.var[:] = args.sigma ** 2
     p.nburn, p.keepk = args.warmup, max(1, args.steps)
-    smp = mcmc.Sampler(p, nchains=hi - lo, chain_offset=lo, v0=v0, max_samples=1, device=local_rank)
+    smp = mcmc.Sampler(p, nchains=hi - lo, chain_offset=lo, v0=v0, max_samples=1, device=local_rank,
+                       precision=args.precision)
     stream = torch.cuda.current_stream(dev)
     smp.set_stream(stream.cuda_stream)
 
@@ -218,16 +221,17 @@ def main():
         n_nodes = p.nx * p.ny * p.nz
         total = per_gpu * world * args.steps
         from mceik_amd import _lib
-        b = _lib.FsmBatch(); b.precision = 32; b.slow_mode = 1; b.nstat = p.nstat
+        b = _lib.FsmBatch(); b.precision = args.precision; b.slow_mode = 1; b.nstat = p.nstat
         b.nrx, b.nry, b.nrz = p.nref
         bpn = _lib.lib().mceik_fsm_bytes_per_node_sweep(C.byref(b))
         # the instance the sampler launches (same batch geometry as mceik_mcmc_init)
         b.nx, b.ny, b.nz, b.h = p.nx, p.ny, p.nz, p.h
-        b.nmodel, b.nsrc, b.fast_sqrt, b.maxit, b.tol = per_gpu, 1, 1, p.maxit, p.tol
+        b.nmodel, b.nsrc, b.fast_sqrt, b.maxit, b.tol = per_gpu, 1, int(args.precision == 32), p.maxit, p.tol
         b.nev = p.nevents
         step_z = _lib.lib().mceik_fsm_step_z(C.byref(b))
         kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
-                 "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)")
+                 "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)"
+                 if args.precision == 32 else "fsm_solve_kernel<double, ...> (8-z steps, fp64 literal update)")
         # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
         # inputs did not change since their last visit are skipped)
         nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
@@ -241,7 +245,7 @@ def main():
             with open(tf) as f:
                 tj = json.load(f)
             if (tj.get("workload") == args.config and tj.get("chains_per_gpu") == per_gpu
-                    and tj.get("kernel_rev") == KERNEL_REV):
+                    and tj.get("kernel_rev") == KERNEL_REV and args.precision == 32):
                 traffic = tj.get("hbm_bytes_per_launch")
         line = {
             "metric": METRIC,
@@ -254,7 +258,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.precision == 32 else "f64",
             "data": f"synthetic (SURVEY s.8d heterogeneous model, picks = GPU forward of the true model + "
                     f"N(0, {args.sigma} s), varObs = {args.sigma}^2)",
             "config": {"workload": f"{args.config}: {per_gpu} chains/GPU, {p.nx}^3 grid, {p.nstat} stations, "

@@ -6,6 +6,10 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
+#ifndef MCEIK_SQRT_INT
+#define MCEIK_SQRT_INT 1     // sqrt_normal's rounding choice in integer arithmetic (0: compares + selects)
+#endif
+
 namespace {
 
 template <typename R> struct Num;
@@ -59,15 +63,33 @@ __device__ __forceinline__ double godunov(double a, double b, double c, double f
 // h/vmax (checked on the host) and the selected radicand exceeds f^2 (2D:
 // 2f^2 - d2^2 with d2 < f; 3D: 3f^2 - (d2^2 + (d3^2 + (d3-d2)^2)) with both
 // terms < f^2).
+//
+// The choice among dn = s - 1 ulp, s, up = s + 1 ulp (LLVM's: edn <= 0 -> dn,
+// eup > 0 -> up, else s; eup > 0 implies edn > 0) is made in integer
+// arithmetic: result bits = dn + [eup > 0] + [edn > 0], each [v > 0] the
+// clamp med3_i32(bits(v), 0, 1) (v is finite: a positive float has positive
+// bits, +-0 and negatives do not).  Same values as the compare/select form
+// without its compare -> lane-mask -> select hazard wait states (gfx950 puts
+// two wait states between a VALU write of an SGPR mask and its use).
 __device__ __forceinline__ float sqrt_normal(float x)
 {
     const float s = __builtin_amdgcn_sqrtf(x);
-    const float dn = __builtin_bit_cast(float, __builtin_bit_cast(int, s) - 1);
-    const float up = __builtin_bit_cast(float, __builtin_bit_cast(int, s) + 1);
-    const float edn = __builtin_fmaf(-dn, s, x);
-    const float eup = __builtin_fmaf(-up, s, x);
-    const float t = edn <= 0.0f ? dn : s;
-    return eup > 0.0f ? up : t;
+    const int sb = __builtin_bit_cast(int, s);
+    const float dn = __builtin_bit_cast(float, sb - 1);
+    const float up = __builtin_bit_cast(float, sb + 1);
+    const int edn = __builtin_bit_cast(int, __builtin_fmaf(-dn, s, x));
+    const int eup = __builtin_bit_cast(int, __builtin_fmaf(-up, s, x));
+#if MCEIK_SQRT_INT
+    // (asm: the instruction selector turns the clamp back into compares + carry adds)
+    int pdn, pup, r;
+    asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pdn) : "v"(edn));
+    asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pup) : "v"(eup));
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(sb - 1), "v"(pdn), "v"(pup));
+    return __builtin_bit_cast(float, r);
+#else
+    const float t = __builtin_bit_cast(float, edn) <= 0.0f ? dn : s;
+    return __builtin_bit_cast(float, eup) > 0.0f ? up : t;
+#endif
 }
 
 // Branchless fp32 Godunov update, values and ierr identical to the twin
