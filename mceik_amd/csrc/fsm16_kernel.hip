@@ -80,7 +80,7 @@ __device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char 
 // Neighbour rows (element offsets into S.xr): array arr (0 = XR: a lane's
 // results of its last step; 1 = XN: its next brick), quarter q (4 z), row
 // (lane 0..63, halo rows 64..79 as in fsm_kernel.hip).
-#define XROW16(arr, q, row) (((((arr) * 4 + (q)) * MCEIK_XROWS) + (row)) * 4)
+#define XROW16(arr, q, row) (((arr) * 4 + (q)) * MCEIK_X16Q + (row) * 4)
 typedef float f4v16 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void lds_w4(float *p, float a, float b, float c, float d)
 {
@@ -179,7 +179,7 @@ __device__ __forceinline__ void seg_finish(const float (&a)[16], float (&v)[16])
 // even's q1, even's q3, own q1, own q3, i.e. base pair_row(arr) + {0, 2Q, 4,
 // 2Q + 4} floats -- and a paired store reads its operands back the same way
 // from the XR rows (raw_read), so both lanes of an instruction hit one line.
-#define XQE (MCEIK_XROWS * 4)    // floats per quarter array
+#define XQE MCEIK_X16Q           // floats per quarter array
 __device__ __forceinline__ int pair_row(int arr, int lane)
 {
     return (lane & 1) ? XROW16(arr, 1, lane - 1) : XROW16(arr, 0, lane);

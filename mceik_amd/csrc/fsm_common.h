@@ -168,10 +168,17 @@ static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t
 // 5 ring: entry int [nr], block id int [nr], tile base u32 [nr] | 6 scratch |
 // 7 neighbour rows XR then XN, each [4 quarters][80 rows][4] float | 8 column meta u32 [nr][64]
 #define MCEIK_SMEM16_ARRAYS 9
+// floats per quarter array of the neighbour rows: 80 rows of 4 plus a 16-B pad,
+// so that the x-pair exchange (even lane: quarter 0, odd lane: quarter 1 of the
+// same row) falls in different LDS banks (unpadded, 320 floats = 5 x 64 banks)
+#ifndef MCEIK_X16PAD
+#define MCEIK_X16PAD 4
+#endif
+#define MCEIK_X16Q (MCEIK_XROWS * 4 + MCEIK_X16PAD)
 #define F16_NR (1 + (15 + MCEIK_AHEAD16 + 1) / 2)      // nr at kb16 = 2
 #define F16_CINFO 0
 #define F16_XR (F16_CINFO + F16_NR * 64 * 4)
-#define F16_CC (F16_XR + 2 * 4 * MCEIK_XROWS * 16)
+#define F16_CC (F16_XR + 2 * 4 * MCEIK_X16Q * 4)
 #define F16_RING (F16_CC + F16_NR * 32 * 4)
 #define F16_SCRATCH (F16_RING + 128)
 #define F16_LASTPROC (F16_SCRATCH + MCEIK_SCRATCH_BYTES)
@@ -200,7 +207,7 @@ static inline __host__ __device__ size_t fsm16_smem_layout(const FsmLaunch &L, s
     off[4] = o; o += mceik_align16(nb * 2);
     off[5] = o; o += mceik_align16(nr * 12);
     off[6] = o; o += MCEIK_SCRATCH_BYTES;
-    off[7] = o; o += 2 * 4 * MCEIK_XROWS * 16;
+    off[7] = o; o += 2 * 4 * MCEIK_X16Q * 4;
     off[8] = o; o += nr * 64 * 4;
     return o;
 }
