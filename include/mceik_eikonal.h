@@ -149,6 +149,18 @@ typedef struct mceik_fsm_batch {
                                    lowest corner is ev_node (fp32, x then y then z, a + w*(b - a)) */
 } mceik_fsm_batch;
 
+/* The batched extension of SURVEY s.8b with plain arguments: nmodels x
+ * nstations single-source solves in one call, fp32 (the sampler's
+ * arithmetic: bitwise the fp32 twin, within 1e-6 u + 1e-7 s of the fp64
+ * reference).  src [nstations][4] = (ts, xs, ys, zs); slow [nmodels][nx*ny*nz]
+ * s/m and u [nmodels*nstations][nx*ny*nz] x fastest, solve m*nstations + s;
+ * niter, ierr [nmodels*nstations] or NULL.  Host or device pointers (host
+ * arrays are staged); synchronous; allocates per call (use
+ * mceik_fsm_batch_solve with a kept workspace for repeated calls).  0 = ok. */
+int eikonal3d_batch_solve(int nmodels, int nstations, int nx, int ny, int nz, double h, double x0, double y0,
+                          double z0, int maxit, double tol, const double *src, const float *slow, float *u,
+                          int *niter, int *ierr);
+
 /* Device workspace (bytes) a launch of this batch needs. */
 size_t mceik_fsm_workspace_bytes(const mceik_fsm_batch *b);
 /* Enqueue the batch on `stream` (hipStream_t; NULL = default).  No host

@@ -78,7 +78,7 @@ class McmcOpts(C.Structure):
 
 
 # every extern "C" symbol include/*.h declares
-EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_initialize", "eikonal3d_solve",
+EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_batch_solve", "eikonal3d_initialize", "eikonal3d_solve",
            "eikonal3d_finalize", "locate3d_gridsearch__double64", "locate3d_gridsearch__float64",
            "locate_l2_gridSearch__double64",
            "locate_l2_gridSearch__float64", "mceik_relocate",
@@ -117,6 +117,8 @@ def lib():
         f.argtypes = [pi] * 4 + [C.c_void_p] * 5 + [pi]
     L.locate_l2_gridSearch__double64.restype = C.c_int
     L.locate_l2_gridSearch__double64.argtypes = [C.c_int] * 4 + [C.c_double] + [C.c_void_p] * 7
+    L.eikonal3d_batch_solve.restype = C.c_int
+    L.eikonal3d_batch_solve.argtypes = [C.c_int] * 5 + [C.c_double] * 4 + [C.c_int, C.c_double] + [C.c_void_p] * 5
     L.mceik_fsm_workspace_bytes.restype = C.c_size_t
     L.mceik_fsm_workspace_bytes.argtypes = [C.POINTER(FsmBatch)]
     L.mceik_fsm_step_z.restype = C.c_int

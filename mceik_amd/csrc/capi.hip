@@ -283,6 +283,65 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
     return 0;
 }
 
+// The plain-argument batched extension SURVEY s.8b names: nmodels x
+// nstations single-source solves (fp32, the sampler's arithmetic) of
+// per-node slowness fields in one call.  Pointers may be host or device
+// memory (host arrays are staged); synchronous.  Solve m*nstations + s
+// uses model m and station s.
+static bool is_device_ptr(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+extern "C" int eikonal3d_batch_solve(int nmodels, int nstations, int nx, int ny, int nz, double h, double x0,
+                                     double y0, double z0, int maxit, double tol, const double *src,
+                                     const float *slow, float *u, int *niter, int *ierr)
+{
+    if (nmodels < 1 || nstations < 1 || !src || !slow || !u) return 1;
+    const size_t n = (size_t)nx * ny * nz, nsolve = (size_t)nmodels * nstations;
+    mceik_fsm_batch b;
+    memset(&b, 0, sizeof(b));
+    b.nx = nx; b.ny = ny; b.nz = nz; b.h = h; b.x0 = x0; b.y0 = y0; b.z0 = z0;
+    b.maxit = maxit; b.tol = tol; b.precision = 32;
+    b.nmodel = nmodels; b.nstat = nstations; b.nsrc = 1; b.slow_mode = 0; b.max_sweeps = -1;
+    std::vector<void *> tmp;
+    auto stage = [&](const void *p, size_t bytes, bool in) -> void * {
+        if (is_device_ptr(p)) return const_cast<void *>(p);
+        void *d = nullptr;
+        if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+        tmp.push_back(d);
+        if (in && hipMemcpy(d, p, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return d;
+    };
+    int rc = 0;
+    void *d_src = stage(src, (size_t)nstations * 4 * sizeof(double), true);
+    void *d_slow = stage(slow, (size_t)nmodels * n * sizeof(float), true);
+    void *d_u = stage(u, nsolve * n * sizeof(float), false);
+    void *d_it = niter ? stage(niter, nsolve * sizeof(int), false) : nullptr;
+    void *d_ie = ierr ? stage(ierr, nsolve * sizeof(int), false) : nullptr;
+    void *ws = nullptr;
+    if (!d_src || !d_slow || !d_u || (niter && !d_it) || (ierr && !d_ie)) rc = -1;
+    if (!rc) {
+        b.src = (const double *)d_src; b.slow = d_slow; b.u_out = d_u;
+        b.niter = (int *)d_it; b.ierr = (int *)d_ie;
+        const size_t wsb = mceik_fsm_workspace_bytes(&b);
+        if (hipMalloc(&ws, wsb) != hipSuccess) rc = -1;
+        else rc = mceik_fsm_batch_solve(&b, ws, wsb, nullptr);
+        if (!rc && hipDeviceSynchronize() != hipSuccess) rc = -1;
+    }
+    if (!rc && d_u != u) rc = hipMemcpy(u, d_u, nsolve * n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess;
+    if (!rc && niter && d_it != niter) rc = hipMemcpy(niter, d_it, nsolve * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess;
+    if (!rc && ierr && d_ie != ierr) rc = hipMemcpy(ierr, d_ie, nsolve * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess;
+    if (ws) hipFree(ws);
+    for (void *p : tmp) hipFree(p);
+    return rc;
+}
+
 extern "C" int mceik_memcpy(void *dst, const void *src, size_t bytes, int kind)
 {
     hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;

@@ -149,3 +149,37 @@ def test_c_sampler_main_config_checkpoint_gather(tmp_path):
     checks = {ln.split()[1]: ln.split()[2] for ln in out.stdout.splitlines() if ln.startswith("check ")}
     assert len(checks) == 6 and all(v == "1" for v in checks.values()), checks
     assert "chains 6 step 8" in out.stdout
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_eikonal3d_batch_solve_plain_arguments(where):
+    """eikonal3d_batch_solve (SURVEY s.8b's batched extension): 2 models x 3
+    stations of per-node slowness, host or device arrays, every field, niter
+    and ierr bitwise = the fp32 twin."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+    from mceik_amd import _lib
+    nx, ny, nz, h, nm, ns = 26, 21, 30, 100.0, 2, 3
+    rng = np.random.default_rng(17)
+    slow = (1.0 / rng.uniform(2500.0, 6500.0, (nm, nz, ny, nx))).astype(np.float32)
+    src = np.stack([np.zeros(ns), rng.uniform(100, (nx - 2) * h, ns), rng.uniform(100, (ny - 2) * h, ns),
+                    rng.uniform(100, (nz - 2) * h, ns)], 1)
+    u = np.zeros((nm * ns, nz, ny, nx), np.float32)
+    it = np.zeros(nm * ns, np.int32)
+    ie = np.full(nm * ns, 7, np.int32)
+    L = _lib.lib()
+    if where == "host":
+        args = [src.ctypes.data, slow.ctypes.data, u.ctypes.data, it.ctypes.data, ie.ctypes.data]
+    else:
+        t = [torch.tensor(a, device="cuda:0") for a in (src, slow, u, it, ie)]
+        args = [x.data_ptr() for x in t]
+    assert L.eikonal3d_batch_solve(nm, ns, nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, *args) == 0
+    if where == "device":
+        u, it, ie = t[2].cpu().numpy(), t[3].cpu().numpy(), t[4].cpu().numpy()
+    for m in range(nm):
+        for s in range(ns):
+            tw, ierr, nit = O.eikonal_solve(nx, ny, nz, slow[m].ravel(), h, src[s], dtype=np.float32)
+            k = m * ns + s
+            assert np.array_equal(u[k].ravel().view(np.uint32), tw.view(np.uint32)), (m, s)
+            assert it[k] == nit and ie[k] == ierr == 0
