@@ -183,3 +183,29 @@ def test_eikonal3d_batch_solve_plain_arguments(where):
             k = m * ns + s
             assert np.array_equal(u[k].ravel().view(np.uint32), tw.view(np.uint32)), (m, s)
             assert it[k] == nit and ie[k] == ierr == 0
+
+
+def test_c_mpi_sampler_main_one_rank(tmp_path):
+    """tests/c/mpi_sampler_main.c under mpiexec -n 1: problem broadcast from
+    rank 0 (broadcast.c's role), chains sharded by rank, RCCL id over
+    MPI_Bcast, the kept states gathered to rank 0 by mceik_mcmc_gather.  (RCCL
+    takes one rank per GPU: more ranks need more GPUs.)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mpi = "/opt/conda"
+    if not (os.path.exists(f"{mpi}/bin/mpiexec") and os.path.exists(f"{mpi}/lib/libmpi.so")):
+        pytest.skip("no MPI toolchain in this image")
+    exe = str(tmp_path / "mpi_sampler_main")
+    lib = os.path.join(ROOT, "mceik_amd")
+    # the system libstdc++ ahead of conda's (libamdhip64 needs the newer one)
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), "-I", f"{mpi}/include",
+                    os.path.join(ROOT, "tests", "c", "mpi_sampler_main.c"), "-L", lib, "-lmceik_hip",
+                    f"{mpi}/lib/libmpi.so", f"-Wl,-rpath,/usr/lib/x86_64-linux-gnu:{lib}:{mpi}/lib", "-lm",
+                    "-o", exe], check=True)
+    out = subprocess.run([f"{mpi}/bin/mpiexec", "-n", "1", exe, "grid:nx=24", "grid:ny=20", "grid:nz=28",
+                          "grid:dx=100", "grid:dy=100", "grid:dz=100", "grid:nrefx=4", "grid:nrefy=4",
+                          "grid:nrefz=4", "mcmc:nchains=5", "mcmc:niter=4", "mcmc:max_samples=1"],
+                         capture_output=True, text=True, timeout=120)
+    print(out.stdout, out.stderr[-2000:])
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "check gather_own_shard 1" in out.stdout and "ranks 1 chains 5" in out.stdout
