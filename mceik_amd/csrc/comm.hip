@@ -102,6 +102,7 @@ struct mceik_comm {
     ncclComm_t comm;
     int nranks, rank, device;
     int *d_shard;          // [nranks][2] (chain_offset, nchains) exchange buffer
+    hipStream_t stream;    // the gather's own stream (non-blocking)
 };
 
 #define RCCLCHK(x)                                                                         \
@@ -143,6 +144,10 @@ extern "C" int mceik_comm_init(const unsigned char id[MCEIK_COMM_ID_BYTES], int 
     memcpy(&u, id, sizeof(u));
     ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, u, rank);
     hipError_t e = r == ncclSuccess ? hipMalloc(&c->d_shard, (size_t)nranks * 2 * sizeof(int)) : hipSuccess;
+    if (r == ncclSuccess && e == hipSuccess) {
+        e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) hipFree(c->d_shard);
+    }
     if (r != ncclSuccess || e != hipSuccess) {
         fprintf(stderr, "mceik_comm_init: %s\n", r != ncclSuccess ? rccl().GetErrorString(r) : hipGetErrorString(e));
         if (r == ncclSuccess) rccl().CommDestroy(c->comm);
@@ -160,8 +165,10 @@ extern "C" int mceik_comm_finalize(mceik_comm **pc)
     ncclResult_t r;
     {
         DevScope dg(c->device);
-        hipFree(c->d_shard);
+        hipStreamSynchronize(c->stream);
         r = rccl().CommDestroy(c->comm);
+        hipStreamDestroy(c->stream);
+        hipFree(c->d_shard);
     }
     delete c;
     *pc = nullptr;
@@ -184,15 +191,18 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
         return 1;
     }
     DevScope dg(c->device);
-    hipStream_t st = (hipStream_t)sh.stream;
+    // A checkpoint is synchronous: the sampler's queued steps finish first, then
+    // the gather runs on the communicator's own stream with blocking host copies.
+    HIPCHK2(hipStreamSynchronize((hipStream_t)sh.stream));
+    hipStream_t st = c->stream;
     // 1. every rank learns every shard (a rank without a kept state sends count -1)
     const int mine[2] = {sh.chain_offset, have ? sh.nchains : -1};
     std::vector<int> all((size_t)c->nranks * 2);
     int rc = 0;
-    HIPCHK2(hipMemcpyAsync(c->d_shard + 2 * c->rank, mine, sizeof(mine), hipMemcpyHostToDevice, st));
+    HIPCHK2(hipMemcpy(c->d_shard + 2 * c->rank, mine, sizeof(mine), hipMemcpyHostToDevice));
     RCCLCHK(rccl().AllGather(c->d_shard + 2 * c->rank, c->d_shard, 2, ncclInt32, c->comm, st));
-    HIPCHK2(hipMemcpyAsync(all.data(), c->d_shard, all.size() * sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK2(hipStreamSynchronize(st));
+    HIPCHK2(hipMemcpy(all.data(), c->d_shard, all.size() * sizeof(int), hipMemcpyDeviceToHost));
     {   // the shards must tile [0, nchains_total): every rank checks the same table
         std::vector<int> cover((size_t)nchains_total, 0);
         for (int r = 0; r < c->nranks && !rc; r++) {
@@ -209,6 +219,7 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
         }
     }
     const size_t ncell = (size_t)sh.ncell;
+    const size_t vbytes = (size_t)nchains_total * ncell * sizeof(int), lbytes = (size_t)nchains_total * sizeof(double);
     // root: receive straight into caller device memory on this GPU, else into a staging buffer
     int *d_v = nullptr;
     double *d_l = nullptr;
@@ -216,37 +227,45 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
     if (c->rank == root) {
         stage_v = !on_device(v_out, c->device);
         stage_l = !on_device(logl_out, c->device);
-        if (stage_v) HIPCHK2(hipMallocAsync((void **)&d_v, (size_t)nchains_total * ncell * sizeof(int), st));
+        if (stage_v) HIPCHK2(hipMalloc((void **)&d_v, vbytes));
         else d_v = v_out;
-        if (stage_l) HIPCHK2(hipMallocAsync((void **)&d_l, (size_t)nchains_total * sizeof(double), st));
-        else d_l = logl_out;
+        if (stage_l && hipMalloc((void **)&d_l, lbytes) != hipSuccess) {
+            if (stage_v) hipFree(d_v);
+            return -1;
+        }
+        if (!stage_l) d_l = logl_out;
     }
-    // 2. shards to the root
-    RCCLCHK(rccl().GroupStart());
+    // 2. shards to the root (one RCCL group), the root's own by a device copy
+    bool ok = rccl().GroupStart() == ncclSuccess;
     if (c->rank == root) {
-        for (int r = 0; r < c->nranks; r++) {
+        for (int r = 0; r < c->nranks && ok; r++) {
             if (r == root) continue;
             const size_t off = (size_t)all[2 * r], n = (size_t)all[2 * r + 1];
-            RCCLCHK(rccl().Recv(d_v + off * ncell, n * ncell, ncclInt32, r, c->comm, st));
-            RCCLCHK(rccl().Recv(d_l + off, n, ncclFloat64, r, c->comm, st));
+            ok = rccl().Recv(d_v + off * ncell, n * ncell, ncclInt32, r, c->comm, st) == ncclSuccess &&
+                 rccl().Recv(d_l + off, n, ncclFloat64, r, c->comm, st) == ncclSuccess;
         }
     } else {
-        RCCLCHK(rccl().Send(sh.v, (size_t)sh.nchains * ncell, ncclInt32, root, c->comm, st));
-        RCCLCHK(rccl().Send(sh.logl, (size_t)sh.nchains, ncclFloat64, root, c->comm, st));
+        ok = rccl().Send(sh.v, (size_t)sh.nchains * ncell, ncclInt32, root, c->comm, st) == ncclSuccess &&
+             rccl().Send(sh.logl, (size_t)sh.nchains, ncclFloat64, root, c->comm, st) == ncclSuccess;
     }
-    RCCLCHK(rccl().GroupEnd());
-    if (c->rank == root) {
+    ok = (rccl().GroupEnd() == ncclSuccess) && ok;
+    if (ok && c->rank == root) {
         const size_t off = (size_t)sh.chain_offset;
-        HIPCHK2(hipMemcpyAsync(d_v + off * ncell, sh.v, (size_t)sh.nchains * ncell * sizeof(int),
-                               hipMemcpyDeviceToDevice, st));
-        HIPCHK2(hipMemcpyAsync(d_l + off, sh.logl, (size_t)sh.nchains * sizeof(double), hipMemcpyDeviceToDevice, st));
-        if (stage_v && v_out)
-            HIPCHK2(hipMemcpyAsync(v_out, d_v, (size_t)nchains_total * ncell * sizeof(int), hipMemcpyDefault, st));
-        if (stage_l && logl_out)
-            HIPCHK2(hipMemcpyAsync(logl_out, d_l, (size_t)nchains_total * sizeof(double), hipMemcpyDefault, st));
-        if (stage_v) HIPCHK2(hipFreeAsync(d_v, st));
-        if (stage_l) HIPCHK2(hipFreeAsync(d_l, st));
+        ok = hipMemcpyAsync(d_v + off * ncell, sh.v, (size_t)sh.nchains * ncell * sizeof(int),
+                            hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(d_l + off, sh.logl, (size_t)sh.nchains * sizeof(double), hipMemcpyDeviceToDevice,
+                            st) == hipSuccess;
     }
-    HIPCHK2(hipStreamSynchronize(st));
+    ok = (hipStreamSynchronize(st) == hipSuccess) && ok;
+    if (ok && c->rank == root) {
+        if (stage_v && v_out) ok = hipMemcpy(v_out, d_v, vbytes, hipMemcpyDeviceToHost) == hipSuccess;
+        if (ok && stage_l && logl_out) ok = hipMemcpy(logl_out, d_l, lbytes, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    if (stage_v) hipFree(d_v);
+    if (stage_l) hipFree(d_l);
+    if (!ok) {
+        fprintf(stderr, "mceik_mcmc_gather: RCCL or copy failure\n");
+        return -1;
+    }
     return 0;
 }
