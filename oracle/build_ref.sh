@@ -13,6 +13,8 @@
 #    supplies those two macros and the include is satisfied from an empty dir.
 #    Built without -fopenmp (locate.c:1308 does not compile under it).
 #  * xgridsearch : gridsearch.f90 main program (known-answer: optimum 21124).
+#  * mpi_ref_driver : oracle/mpi_ref_driver.c (ours) calling the reference's
+#    MPI-variant solver on a block decomposition, for tests/golden/blocks_mpi.npz.
 # Nothing from /root/reference is copied into the repository.
 set -euo pipefail
 R=${REFERENCE_DIR:-/root/reference}
@@ -32,6 +34,10 @@ $F -shared -fPIC -fopenmp -o libfsm3d_ref.so mod/mpimod.o mod/module.o mod/mpiut
 # the reference's own MPI test program (xfsm3d main, fsm3d.f90:2055-2183)
 $F -O2 -fopenmp -o xfsm3d mod/mpimod.o mod/module.o mod/mpiutils.o mod/fsm3d.o \
    -L/opt/conda/lib -Wl,-rpath,/opt/conda/lib -Wl,-rpath,/opt/rocm/lib/llvm/lib -lmpifort -lmpi
+# golden generator for the MPI variant (our test driver oracle/mpi_ref_driver.c,
+# linked against the reference build above; run under mpiexec by make_golden.py)
+gcc -O1 -I/opt/conda/include "$HERE/mpi_ref_driver.c" -o mpi_ref_driver -L"$OUT" -lfsm3d_ref /opt/conda/lib/libmpi.so \
+    -Wl,-rpath,"$OUT":/usr/lib/x86_64-linux-gnu:/opt/conda/lib:/opt/rocm/lib/llvm/lib
 : > inc/lapacke_utils.h
 gcc -O2 -fPIC -shared -I inc -I/opt/conda/include '-DMIN(a,b)=((a)<(b)?(a):(b))' '-DMAX(a,b)=((a)>(b)?(a):(b))' \
     -Dmain=locate_c_unused_main "$R/locate.c" -o liblocate_ref.so -lm 2> inc/locate.warn || { cat inc/locate.warn; exit 1; }

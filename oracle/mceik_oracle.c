@@ -428,3 +428,86 @@ void oracle_mcmc_run(const oracle_mcmc_problem *p, int nchains, uint32_t gid0, u
     }
     free(vp); free(tt);
 }
+
+/* EIKONAL3D_SOLVE of the MPI variant (fsm3d.f90:1754-1852) on an ndivx x
+ * ndivy x ndivz block decomposition, every block in this process:
+ * EIKONAL3D_GHOST_COMM's blocks (fsm3d.f90:1086-1101: nd = max(n/ndiv, 1),
+ * block b owns [nd*b, nd*(b+1)-1], the last block up to n-1; a ghost layer of
+ * width noverlap), EIKONAL3D_FSM_MPI's loop (:103-222): per sweep every block
+ * runs its own Gauss-Seidel sweep over its nodes (ghosts and BC nodes are not
+ * updated) reading ghost values as they were at the sweep's start, then
+ * EIKONAL_EXCHANGE (:971-1046) refreshes the ghosts; with noverlap = 0 a block
+ * face is a grid edge (GET_U*MIN3D's one-sided rule).  Convergence: every
+ * owned node |u0-u| < tol.  ierr: the last EVAL_UPDATE3D of rank 0 (block
+ * (0,0,0)): the update ierr of node (1,1,1) in the iteration's last sweep.
+ * Pinned against the reference's own MPI runs (tests/golden/blocks_mpi.npz). */
+int oracle_eikonal3d_solve_blocks_f64(int maxit, int nsrc, int nx, int ny, int nz, int ndivx, int ndivy,
+                                      int ndivz, int noverlap, double tol, double h, double x0, double y0,
+                                      double z0, const double *ts, const double *xs, const double *ys,
+                                      const double *zs, const double *slow, double *u, int *niter_out)
+{
+    static const int sweeps[8][3] = {{0,0,0},{1,0,0},{0,1,0},{1,1,0},{0,0,1},{1,0,1},{0,1,1},{1,1,1}};
+    const int nn[3] = {nx, ny, nz}, nd[3] = {ndivx, ndivy, ndivz};
+    int step[3];
+    for (int a = 0; a < 3; a++) step[a] = nn[a] / nd[a] > 1 ? nn[a] / nd[a] : 1;
+    size_t n = (size_t)nx * ny * nz, nxy = (size_t)nx * ny;
+    unsigned char *lisbc = (unsigned char *)malloc(n);
+    if (niter_out) *niter_out = 0;
+    int ierr = setbcs_f64(nx, ny, nz, nsrc, h, x0, y0, z0, ts, xs, ys, zs, slow, lisbc, u);
+    if (ierr) { free(lisbc); return ierr; }
+    double *u0 = (double *)malloc(n * sizeof(double)), *snap = (double *)malloc(n * sizeof(double));
+    memcpy(u0, u, n * sizeof(double));
+    int k;
+    for (k = 1; k <= maxit; k++) {
+        for (int sw = 0; sw < 8; sw++) {
+            memcpy(snap, u, n * sizeof(double));
+            for (int bz = 0; bz < ndivz; bz++)
+            for (int by = 0; by < ndivy; by++)
+            for (int bx = 0; bx < ndivx; bx++) {
+                const int b[3] = {bx, by, bz};
+                int lo[3], hi[3];
+                for (int a = 0; a < 3; a++) {
+                    lo[a] = step[a] * b[a];
+                    hi[a] = b[a] + 1 == nd[a] ? nn[a] - 1 : step[a] * (b[a] + 1) - 1;
+                }
+                int last_ierr = 0;
+                for (int kz = 0; kz <= hi[2] - lo[2]; kz++) {
+                    int iz = sweeps[sw][2] ? hi[2] - kz : lo[2] + kz;
+                    for (int ky = 0; ky <= hi[1] - lo[1]; ky++) {
+                        int iy = sweeps[sw][1] ? hi[1] - ky : lo[1] + ky;
+                        for (int kx = 0; kx <= hi[0] - lo[0]; kx++) {
+                            int ix = sweeps[sw][0] ? hi[0] - kx : lo[0] + kx;
+                            size_t ijk = (size_t)iz * nxy + (size_t)iy * nx + ix;
+                            last_ierr = 0;
+                            if (lisbc[ijk]) continue;
+                            double self = u[ijk], f = slow[ijk] * h;
+                            /* neighbour: outside the grid -> self; inside this block -> live;
+                               another block's node -> the ghost (start of sweep), or self
+                               without a ghost layer */
+#define NB(cond_in, inblk, off) (!(cond_in) ? self : (inblk) ? u[ijk + (off)] : (noverlap > 0 ? snap[ijk + (off)] : self))
+                            double xm = NB(ix > 0, ix - 1 >= lo[0], -1), xp = NB(ix < nx - 1, ix + 1 <= hi[0], 1);
+                            double ym = NB(iy > 0, iy - 1 >= lo[1], -(long)nx), yp = NB(iy < ny - 1, iy + 1 <= hi[1], (long)nx);
+                            double zm = NB(iz > 0, iz - 1 >= lo[2], -(long)nxy), zp = NB(iz < nz - 1, iz + 1 <= hi[2], (long)nxy);
+#undef NB
+                            double ux = xm < xp ? xm : xp, uy = ym < yp ? ym : yp, uz = zm < zp ? zm : zp;
+                            int e1;
+                            double ub = solve3d_f64(ux, uy, uz, f, &e1);
+                            last_ierr = e1;
+                            u[ijk] = self < ub ? self : ub;
+                        }
+                    }
+                }
+                if (bx == 0 && by == 0 && bz == 0) ierr = last_ierr;
+            }
+        }
+        size_t lconv = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (fabs(u0[i] - u[i]) < tol) lconv++;
+            u0[i] = u[i];
+        }
+        if (lconv == n) break;
+    }
+    if (niter_out) *niter_out = (k > maxit ? maxit : k);
+    free(u0); free(snap); free(lisbc);
+    return ierr;
+}

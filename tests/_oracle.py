@@ -68,6 +68,23 @@ def eikonal_solve(nx, ny, nz, slow, h, sources, maxit=50, tol=1e-8, x0=0.0, y0=0
     return u, ierr, it.value
 
 
+def eikonal_solve_blocks(nx, ny, nz, slow, h, src, ndiv, noverlap, maxit=50, tol=1e-8, x0=0.0, y0=0.0, z0=0.0):
+    """oracle_eikonal3d_solve_blocks_f64: the MPI variant's block-decomposed
+    solve (fp64).  Returns (u, ierr, niter)."""
+    L = lib()
+    f = L.oracle_eikonal3d_solve_blocks_f64
+    f.restype = C.c_int
+    f.argtypes = [C.c_int] * 9 + [C.c_double] * 5 + [C.c_void_p] * 7
+    src = np.atleast_2d(np.asarray(src, dtype=np.float64))
+    cols = [np.ascontiguousarray(src[:, k]) for k in range(4)]
+    slow = np.ascontiguousarray(slow, dtype=np.float64)
+    u = np.zeros(nx * ny * nz)
+    it = C.c_int(0)
+    ierr = f(maxit, len(cols[0]), nx, ny, nz, *ndiv, noverlap, tol, h, x0, y0, z0, *[_p(c) for c in cols],
+             _p(slow), _p(u), C.byref(it))
+    return u, ierr, it.value
+
+
 def locate_l2(ldgrd, ngrd, nobs, iwant, t0use, mask, tobs, tcorr, varobs, test):
     t0 = np.zeros(ngrd); obj = np.zeros(ngrd)
     m = np.ascontiguousarray(mask, dtype=np.int32)

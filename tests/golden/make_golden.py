@@ -250,9 +250,62 @@ def make_locate():
     np.savez_compressed(os.path.join(HERE, "locate_l2_f32.npz"), **o32)
 
 
+def make_fsm_mpi():
+    """The reference's MPI-variant solver (EIKONAL3D_INITIALIZE/_SOLVE,
+    fsm3d.f90:1583-1852) on block decompositions, one MPI rank per block,
+    through oracle/_ref/mpi_ref_driver (mpiexec).  The reference accepts
+    1- or 2-way splits per axis here (3- and 4-way splits abort in its
+    initialisation).  Fields are stored for the small grid; the xfsm3d
+    70x80x90 case stores a digest, max u and the iteration-count-free ierr."""
+    import subprocess
+    import tempfile
+    drv = os.path.join(REF, "mpi_ref_driver")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    nx, ny, nz, h = 20, 18, 22, 100.0
+    slow = np.ascontiguousarray((1.0 / hetero_velocity(nx, ny, nz)).ravel())
+    src = (0.0, 834.5, 987.6, 1100.0)
+    cases = [("b211", (2, 1, 1), 1, 50, src), ("b222", (2, 2, 2), 1, 50, src), ("b121_ov2", (1, 2, 1), 2, 50, src),
+             ("b112", (1, 1, 2), 1, 50, src), ("b212_ov0", (2, 1, 2), 0, 50, src), ("b221_ov0", (2, 2, 1), 0, 50, src),
+             ("b222_maxit1", (2, 2, 2), 1, 1, src), ("b222_onnode", (2, 2, 2), 1, 50, (0.5, 900.0, 800.0, 1000.0)),
+             ("b222_origin_err", (2, 2, 2), 1, 50, (0.0, 0.0, 0.0, 0.0))]
+    out = {"grid": np.array([nx, ny, nz]), "h": h, "slow": slow}
+    with tempfile.TemporaryDirectory() as td:
+        sp, op = os.path.join(td, "slow.f64"), os.path.join(td, "u.f64")
+        slow.tofile(sp)
+        for name, nd, nov, maxit, s in cases:
+            cmd = [mpiexec, "-n", str(nd[0] * nd[1] * nd[2]), drv, str(nx), str(ny), str(nz), *map(str, nd), str(nov),
+                   str(maxit), "1e-8", str(h), "0", "0", "0", *map(repr, s), sp, op]
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            if name.endswith("_err"):
+                # SETBCS fails (source on the first node, fsm3d.f90:736-753): the
+                # solve returns ierr = 1 on every rank before any sweep
+                out[f"{name}_ierr"] = np.int32(1 if r.returncode == 0 and np.fromfile(op)[-1] == 1.0 else -1)
+            else:
+                assert r.returncode == 0, (name, r.stdout[-500:], r.stderr[-500:])
+                res = np.fromfile(op)
+                out[f"{name}_u"], out[f"{name}_ierr"] = res[:-1], np.int32(res[-1])
+            out[f"{name}_cfg"] = np.array([*nd, nov, maxit])
+            out[f"{name}_src"] = np.array(s)
+        # the reference's own xfsm3d case (fsm3d.f90:2085-2100): 70x80x90, 2x2x2 blocks
+        n3 = (70, 80, 90)
+        sl = np.full(n3[0] * n3[1] * n3[2], 1.0 / 5.0e3)
+        sl.tofile(sp)
+        xs = tuple(100.0 * n / 2.0 for n in n3)
+        cmd = [mpiexec, "-n", "8", drv, *map(str, n3), "2", "2", "2", "1", "5", "1e-7", "100", "0", "0", "0", "0",
+               *map(repr, xs), sp, op]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-500:]
+        res = np.fromfile(op)
+        out["xfsm3d_sha256"] = np.array(hashlib.sha256(res[:-1].tobytes()).hexdigest())
+        out["xfsm3d_max"], out["xfsm3d_ierr"] = res[:-1].max(), np.int32(res[-1])
+    np.savez_compressed(os.path.join(HERE, "blocks_mpi.npz"), **out)
+
+
 if __name__ == "__main__":
     if not os.path.exists(os.path.join(REF, "libfsm3d_ref.so")):
         sys.exit("build the reference first: oracle/build_ref.sh")
     make_fsm(RefFSM())
     make_locate()
     make_gridsearch()
+    if os.path.exists(os.path.join(REF, "mpi_ref_driver")) and os.path.exists("/opt/conda/bin/mpiexec"):
+        make_fsm_mpi()
