@@ -372,16 +372,36 @@ struct SingleState {
     // MPI-variant parameters (eikonal3d_initialize)
     int iverb, maxit;
     double x0, y0, z0, h, tol;
+    BlockDecomp D;               // the reference's block decomposition (more than one block: blocks_solve)
+    double *snap;                // ghost copies: u at the start of the sweep (padded layout)
+    unsigned *d_count;           // unconverged-node count
 };
 static SingleState g_single[3];          // [0] serial fp32, [1] serial fp64, [2] MPI variant (fp64)
 
+// Frees the device state; the caller's parameters (init flag, the MPI
+// variant's eikonal3d_initialize arguments and decomposition) survive.
 static void single_free(SingleState &S)
 {
+    if (S.snap) hipFree(S.snap);
+    if (S.d_count) hipFree(S.d_count);
     if (S.mem) hipFree(S.mem);
     if (S.st) hipStreamDestroy(S.st);
-    const int keep = S.init;
+    const SingleState keep = S;
     memset(&S, 0, sizeof(S));
-    S.init = keep;
+    S.init = keep.init;
+    S.iverb = keep.iverb; S.maxit = keep.maxit;
+    S.x0 = keep.x0; S.y0 = keep.y0; S.z0 = keep.z0; S.h = keep.h; S.tol = keep.tol;
+    S.D = keep.D;
+}
+
+// Ghost snapshot and counters of the block-decomposed solve (allocated once
+// per grid; single_alloc reallocations drop them).
+static int blocks_buffers(SingleState &S)
+{
+    const size_t np = (size_t)S.L.nxp * S.L.nyp * S.L.nzp;
+    if (!S.snap && hipMalloc(&S.snap, np * 8) != hipSuccess) { S.snap = nullptr; return 1; }
+    if (!S.d_count && hipMalloc(&S.d_count, 16) != hipSuccess) { S.d_count = nullptr; return 1; }
+    return 0;
 }
 
 // Device buffers of a solve on nx x ny x nz (maxit iterations, nsrc sources).
@@ -578,24 +598,93 @@ extern "C" void eikonal3d_serial_driver_sp(const int *job, const int *iverb, con
 
 // MPI variant (fsm3d.f90:1583-1929) on one GPU.  The reference decomposes the
 // grid over ndivx*ndivy*ndivz ranks of `comm` and gathers u on rank 0; here
-// the whole grid lives on the calling process's GPU, so the decomposition
-// arguments and `comm` are accepted and not used.  Collective semantics are
-// kept by the reference's own convention: the master passes the full arrays
-// (n = nx*ny*nz) and gets the travel times; every other rank passes n < nx*ny*nz
-// (the reference's callers use n = 1, fsm3d.f90:2102-2106) and returns at once
-// with ierr = 0.  Computes in fp64 with the serial driver's arithmetic, so u is
-// the Gauss-Seidel fixed point the reference's decomposed solve converges to
-// (xfsm3d: max u = 1.4308203212738235 from both).
+// the whole grid lives on the calling process's GPU and `comm` is not used,
+// but the decomposition is: with more than one block the solve runs the
+// reference's block-decomposed iteration (blocks_solve: per sweep every block
+// sweeps its own nodes against ghost copies refreshed after the sweep), so u,
+// the iteration count and ierr are bitwise those of the reference's run with
+// one MPI rank per block (tests/golden/blocks_mpi.npz); one block is the
+// serial driver's solve.  Collective semantics are kept by the reference's own
+// convention: the master passes the full arrays (n = nx*ny*nz) and gets the
+// travel times; every other rank passes n < nx*ny*nz (the reference's callers
+// use n = 1, fsm3d.f90:2102-2106) and returns at once with ierr = 0.
+// The block-decomposed solve of the MPI variant on one GPU (EIKONAL3D_FSM_MPI,
+// fsm3d.f90:103-222; fsm_single.hip block_sweep_kernel): SETBCS, then per
+// iteration 8 sweeps, each preceded by the ghost snapshot (the state every
+// block's EIKONAL_EXCHANGE leaves), then the convergence count.  Returns the
+// reference's ierr (rank 0's) or -1 on a device failure.
+static int blocks_solve(SingleState &S, int nsrc, const double *ts, const double *xs, const double *ys,
+                        const double *zs, const double *slow, double *u, int *niter_out)
+{
+    SingleLaunch &L = S.L;
+    const size_t n = (size_t)L.nx * L.ny * L.nz, np = (size_t)L.nxp * L.nyp * L.nzp;
+    L.maxit = S.maxit; L.tol = S.tol; L.h = S.h; L.x0 = S.x0; L.y0 = S.y0; L.z0 = S.z0;
+    std::vector<double> src((size_t)nsrc * 4);
+    for (int k = 0; k < nsrc; k++) {
+        src[k * 4 + 0] = ts[k]; src[k * 4 + 1] = xs[k]; src[k * 4 + 2] = ys[k]; src[k * 4 + 3] = zs[k];
+    }
+    hipStream_t st = S.st;
+    int ierr_bc = 0, ierr = 0, niter = 0;
+    if (hipMemcpyAsync(S.dense, slow, n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(S.src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        fsm_single_pad(S.dense, (void *)L.slow, 1, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
+        fsm_single_setbcs(L, S.src, nsrc, S.ierr_bc, st) != hipSuccess ||
+        hipMemcpyAsync(&ierr_bc, S.ierr_bc, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return -1;
+    S.bcfail = ierr_bc != 0;
+    int *d_ierr = (int *)(S.d_count + 1);
+    for (int k = 1; k <= S.maxit && !ierr_bc; k++) {
+        niter = k;
+        if (hipMemcpyAsync(L.u0, L.u, np * 8, hipMemcpyDeviceToDevice, st) != hipSuccess) return -1;
+        for (int g = 0; g < 8; g++)
+            if (hipMemcpyAsync(S.snap, L.u, np * 8, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipMemsetAsync(d_ierr, 0, 4, st) != hipSuccess ||
+                fsm_block_sweep(L, S.D, S.snap, g, d_ierr, st) != hipSuccess)
+                return -1;
+        unsigned count = 0;
+        if (hipMemsetAsync(S.d_count, 0, 4, st) != hipSuccess ||
+            fsm_block_unconverged(L, S.tol, S.d_count, st) != hipSuccess ||
+            hipMemcpyAsync(&count, S.d_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(&ierr, d_ierr, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return -1;
+        if (count == 0) break;
+    }
+    if (fsm_single_unpad(L.u, S.dense, 1, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
+        hipMemcpyAsync(u, S.dense, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return -1;
+    if (niter_out) *niter_out = niter;
+    return ierr_bc ? 1 : ierr;
+}
+
 extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const int *nx, const int *ny, const int *nz,
                                      const int *ndivx, const int *ndivy, const int *ndivz, const int *noverlap,
                                      const int *maxit, const double *x0, const double *y0, const double *z0,
                                      const double *h, const double *tol, int *ierr)
 {
-    (void)comm; (void)ndivx; (void)ndivy; (void)ndivz; (void)noverlap;
+    (void)comm;
     SingleState &S = g_single[2];
     *ierr = 0;
     if (*iverb > 0) printf(" eikonal3d_initialize: Broadcasting parameters...\n");
+    if (*ndivx < 1 || *ndivy < 1 || *ndivz < 1 || *noverlap < 0) {
+        printf(" eikonal3d_initialize: Error computing local domain\n");
+        *ierr = 1;
+        return;
+    }
     if (single_alloc(S, 1, *nx, *ny, *nz, *maxit, 1)) {
+        printf(" eikonal3d_initialize: Error making the device structures\n");
+        *ierr = 1;
+        return;
+    }
+    const int nd[3] = {*ndivx, *ndivy, *ndivz}, nn[3] = {*nx, *ny, *nz};
+    for (int a = 0; a < 3; a++) {
+        S.D.nd[a] = nd[a];
+        S.D.step[a] = nn[a] / nd[a] > 1 ? nn[a] / nd[a] : 1;       // fsm3d.f90:1086-1088
+    }
+    S.D.nov = *noverlap;
+    if (nd[0] * nd[1] * nd[2] > 1 && blocks_buffers(S)) {
         printf(" eikonal3d_initialize: Error making the device structures\n");
         *ierr = 1;
         return;
@@ -616,13 +705,16 @@ extern "C" void eikonal3d_solve(const int *comm, const int *nsrc, const int *n, 
         return;
     }
     if ((long)*n < (long)S.nx * S.ny * S.nz) return;          // not the master: nothing to hold
-    if (*nsrc < 1 || single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, *nsrc)) {
+    const bool blocks = S.D.nd[0] * S.D.nd[1] * S.D.nd[2] > 1;
+    if (*nsrc < 1 || single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, *nsrc) || (blocks && blocks_buffers(S))) {
         printf(" eikonal3d_solve: Error setting bcs\n");
         *ierr = 1;
         return;
     }
     if (S.iverb > 0) printf(" eikonal3d_solve: Setting boundary conditions...\n");
-    const int rc = single_solve(S, S.maxit, *nsrc, S.tol, S.h, S.x0, S.y0, S.z0, ts, xs, ys, zs, slow, u, nullptr);
+    const int rc = blocks ? blocks_solve(S, *nsrc, ts, xs, ys, zs, slow, u, nullptr)
+                          : single_solve(S, S.maxit, *nsrc, S.tol, S.h, S.x0, S.y0, S.z0, ts, xs, ys, zs, slow, u,
+                                         nullptr);
     if (S.bcfail) printf(" eikonal3d_solve: Error setting bcs\n");
     else if (rc != 0) printf(" eikonal3d_solve: Error calling solver\n");
     *ierr = rc < 0 ? 1 : rc;

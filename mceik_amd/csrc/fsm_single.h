@@ -22,7 +22,18 @@ struct SingleLaunch {
     const int *bcerr;                // SETBCS failed (ierr = 1): no sweep runs
 };
 
+// Block decomposition of the MPI variant (fsm3d.f90:1086-1101): nd blocks per
+// axis, block b owning [step*b, step*(b+1)-1] (the last one up to n-1), ghost
+// layer width nov (0: block faces are grid edges).
+struct BlockDecomp {
+    int nd[3], step[3], nov;
+};
+
 int fsm_single_occupancy(int is_double);
+hipError_t fsm_single_setbcs(const SingleLaunch &L, const double *d_src, int nsrc, int *d_ierr_bc, hipStream_t st);
+hipError_t fsm_block_sweep(const SingleLaunch &L, const BlockDecomp &D, const double *snap, int g, int *ierr,
+                           hipStream_t st);
+hipError_t fsm_block_unconverged(const SingleLaunch &L, double tol, unsigned *count, hipStream_t st);
 hipError_t fsm_single_solve(const SingleLaunch &L, int is_double, const double *d_src, int nsrc, int *d_ierr_bc,
                             int nwaves, hipStream_t st);
 hipError_t fsm_single_pad(const double *src, void *dst, int is_double, int nx, int ny, int nz, int nxp, int nyp,

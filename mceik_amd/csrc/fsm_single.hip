@@ -346,7 +346,106 @@ __global__ void single_pad_kernel(const RS *src, RD *dst, int nx, int ny, int nz
     }
 }
 
+// ---- the MPI variant's block decomposition (EIKONAL3D_FSM_MPI) --------------
+// fsm3d.f90:103-222 with EIKONAL3D_GHOST_COMM's blocks (:1086-1101) and
+// EIKONAL_EXCHANGE after every sweep (:971-1046): per sweep every block runs
+// its own Gauss-Seidel sweep over the nodes it owns, reading a neighbour that
+// another block owns as that block's ghost copy, i.e. its value at the start
+// of the sweep (snap), or -- without a ghost layer (noverlap = 0) -- as a
+// missing neighbour (GET_U*MIN3D's one-sided rule: the node itself).  One
+// workgroup per block walks the block's node hyperplanes in sweep order (the
+// nodes of a level are independent), so the result is bitwise the reference's
+// run with one MPI rank per block.  fp64, the padded layout of SingleLaunch.
+__global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockDecomp D, const double *snap, int g,
+                                                          int *ierr)
+{
+    const int b = blockIdx.x;
+    const int bi[3] = {b % D.nd[0], (b / D.nd[0]) % D.nd[1], b / (D.nd[0] * D.nd[1])};
+    const int nn[3] = {L.nx, L.ny, L.nz};
+    int lo[3], ext[3];
+    for (int a = 0; a < 3; a++) {
+        lo[a] = D.step[a] * bi[a];
+        const int hi = bi[a] + 1 == D.nd[a] ? nn[a] - 1 : D.step[a] * (bi[a] + 1) - 1;
+        ext[a] = hi - lo[a] + 1;
+        if (ext[a] <= 0) return;                       // an empty block (more blocks than nodes)
+    }
+    const bool rev[3] = {(g & 1) != 0, (g & 2) != 0, (g & 4) != 0};
+    double *u = (double *)L.u;
+    const double *slow = (const double *)L.slow;
+    const size_t sy = (size_t)L.nxp, sz = (size_t)L.nxp * L.nyp;
+    const int nlev = ext[0] + ext[1] + ext[2] - 2;
+    for (int lev = 0; lev < nlev; lev++) {
+        const int zlo = max(0, lev - (ext[0] - 1) - (ext[1] - 1)), zhi = min(ext[2] - 1, lev);
+        const int npairs = (zhi - zlo + 1) * ext[1];
+        for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
+            const int kz = zlo + p / ext[1], ky = p % ext[1], kx = lev - kz - ky;
+            if (kx < 0 || kx >= ext[0]) continue;
+            const int k3[3] = {kx, ky, kz};
+            int c[3];
+            for (int a = 0; a < 3; a++) c[a] = rev[a] ? lo[a] + ext[a] - 1 - k3[a] : lo[a] + k3[a];
+            const size_t idx = (size_t)c[2] * sz + (size_t)c[1] * sy + (size_t)c[0];
+            if (L.bc[idx]) continue;                   // lupd = .FALSE. (SETBCS node)
+            const double self = u[idx];
+            double nb[6];
+            const size_t stride[3] = {1, sy, sz};
+            for (int a = 0; a < 3; a++)
+                for (int s = 0; s < 2; s++) {
+                    const int q = c[a] + (s ? 1 : -1);
+                    const size_t qi = s ? idx + stride[a] : idx - stride[a];
+                    double v;
+                    if (q < 0 || q >= nn[a]) v = self;                          // outside the grid
+                    else if (q >= lo[a] && q < lo[a] + ext[a]) v = u[qi];        // this block: live
+                    else v = D.nov > 0 ? snap[qi] : self;                        // ghost / no ghost layer
+                    nb[2 * a + s] = v;
+                }
+            const double ux = fmin_(nb[0], nb[1]), uy = fmin_(nb[2], nb[3]), uz = fmin_(nb[4], nb[5]);
+            int e;
+            const double ub = godunov(ux, uy, uz, slow[idx] * L.h, e);
+            u[idx] = self < ub ? self : ub;
+            if (b == 0 && c[0] == 0 && c[1] == 0 && c[2] == 0) *ierr = e;   // rank 0's last EVAL_UPDATE3D
+        }
+        __syncthreads();
+    }
+}
+
+// nodes with !(|u0 - u| < tol) (the FSM_MPI convergence count, fsm3d.f90:195-205)
+__global__ void block_unconverged_kernel(SingleLaunch L, double tol, unsigned *count)
+{
+    const size_t n = (size_t)L.nx * L.ny * L.nz;
+    unsigned c = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % L.nx);
+        const size_t t = i / L.nx;
+        const int y = (int)(t % L.ny), z = (int)(t / L.ny);
+        const size_t p = ((size_t)z * L.nyp + y) * L.nxp + x;
+        const double d = ((const double *)L.u0)[p] - ((const double *)L.u)[p];
+        c += !(__builtin_fabs(d) < tol);
+    }
+    if (c) atomicAdd(count, c);
+}
+
 }  // namespace
+
+hipError_t fsm_single_setbcs(const SingleLaunch &L, const double *d_src, int nsrc, int *d_ierr_bc, hipStream_t st)
+{
+    const size_t np = (size_t)L.nxp * L.nyp * L.nzp;
+    hipLaunchKernelGGL(single_fill_kernel<double>, dim3(1024), dim3(256), 0, st, (double *)L.u, L.bc, np);
+    hipLaunchKernelGGL(single_setbcs_kernel<double>, dim3(1), dim3(64), 0, st, L, d_src, nsrc, d_ierr_bc);
+    return hipGetLastError();
+}
+
+hipError_t fsm_block_sweep(const SingleLaunch &L, const BlockDecomp &D, const double *snap, int g, int *ierr,
+                           hipStream_t st)
+{
+    hipLaunchKernelGGL(block_sweep_kernel, dim3(D.nd[0] * D.nd[1] * D.nd[2]), dim3(256), 0, st, L, D, snap, g, ierr);
+    return hipGetLastError();
+}
+
+hipError_t fsm_block_unconverged(const SingleLaunch &L, double tol, unsigned *count, hipStream_t st)
+{
+    hipLaunchKernelGGL(block_unconverged_kernel, dim3(512), dim3(256), 0, st, L, tol, count);
+    return hipGetLastError();
+}
 
 int fsm_single_occupancy(int is_double)
 {

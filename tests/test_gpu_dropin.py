@@ -209,3 +209,60 @@ def test_c_mpi_sampler_main_one_rank(tmp_path):
     print(out.stdout, out.stderr[-2000:])
     assert out.returncode == 0, out.stdout + out.stderr
     assert "check gather_own_shard 1" in out.stdout and "ranks 1 chains 5" in out.stdout
+
+
+def _blocks_golden():
+    d = np.load(os.path.join(ROOT, "tests", "golden", "blocks_mpi.npz"))
+    return d, sorted({k[:-4] for k in d.files if k.endswith("_cfg")})
+
+
+def _mpi_variant(nx, ny, nz, nd, nov, maxit, tol, h, slow, src):
+    import ctypes as C
+    from mceik_amd import _lib
+    L = _lib.lib()
+    i = lambda v: C.byref(C.c_int(v))
+    d = lambda v: C.byref(C.c_double(v))
+    ierr = C.c_int(0)
+    L.eikonal3d_initialize(i(0), i(0), i(nx), i(ny), i(nz), i(nd[0]), i(nd[1]), i(nd[2]), i(nov), i(maxit),
+                           d(0.0), d(0.0), d(0.0), d(h), d(tol), C.byref(ierr))
+    assert ierr.value == 0
+    n = nx * ny * nz
+    u = np.zeros(n)
+    s = [np.array([v], dtype=np.float64) for v in src]
+    slow = np.ascontiguousarray(slow, dtype=np.float64)
+    L.eikonal3d_solve(i(0), i(1), i(n), *[x.ctypes.data_as(C.POINTER(C.c_double)) for x in s],
+                      slow.ctypes.data_as(C.POINTER(C.c_double)), u.ctypes.data_as(C.POINTER(C.c_double)),
+                      C.byref(ierr))
+    e = ierr.value
+    L.eikonal3d_finalize(i(0), C.byref(ierr))
+    return u, e
+
+
+@pytest.mark.parametrize("case", _blocks_golden()[1])
+def test_mpi_variant_blocks_bitwise_vs_reference_mpi_runs(case):
+    """eikonal3d_initialize/solve/finalize with ndivx x ndivy x ndivz blocks:
+    the block-decomposed FSM (EIKONAL3D_FSM_MPI semantics, one workgroup per
+    block on one GPU) bitwise = the reference's own solver run under mpiexec
+    with one rank per block (tests/golden/blocks_mpi.npz), ierr included."""
+    _dev()
+    d, _ = _blocks_golden()
+    nx, ny, nz = (int(v) for v in d["grid"])
+    cfg = d[f"{case}_cfg"]
+    u, ierr = _mpi_variant(nx, ny, nz, tuple(int(v) for v in cfg[:3]), int(cfg[3]), int(cfg[4]), 1e-8,
+                           float(d["h"]), d["slow"], d[f"{case}_src"])
+    assert ierr == int(d[f"{case}_ierr"])
+    if f"{case}_u" in d.files:
+        assert np.array_equal(u.view(np.uint64), d[f"{case}_u"].view(np.uint64))
+
+
+def test_mpi_variant_blocks_xfsm3d_digest():
+    """The reference's xfsm3d case (70x80x90, 2x2x2 blocks, maxit 5, tol 1e-7):
+    the field's sha256 equals the reference's 8-rank MPI run."""
+    import hashlib
+    _dev()
+    d, _ = _blocks_golden()
+    n = (70, 80, 90)
+    u, ierr = _mpi_variant(*n, (2, 2, 2), 1, 5, 1e-7, 100.0, np.full(n[0] * n[1] * n[2], 1.0 / 5.0e3),
+                           [0.0] + [100.0 * v / 2.0 for v in n])
+    assert ierr == 0 and u.max() == 1.4308203212738235
+    assert hashlib.sha256(u.tobytes()).hexdigest() == str(d["xfsm3d_sha256"])
