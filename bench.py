@@ -174,10 +174,25 @@ def main():
     smp.set_stream(stream.cuda_stream)
 
     comm = post = None
+    gather_path = None
     if world > 1:
         # the library's checkpoint gather (mceik_mcmc_gather, RCCL over xGMI);
-        # the id travels over the torch.distributed group, as MPI_Bcast would carry it
-        comm = mcmc.Comm.from_torch(local_rank)
+        # the id travels over the torch.distributed group, as MPI_Bcast would carry it.
+        # If the library cannot build its communicator on this node, every rank
+        # uses torch.distributed's gather instead (same bytes, same collective)
+        # and the line says so.
+        ok = 1
+        try:
+            comm = mcmc.Comm.from_torch(local_rank)
+        except Exception as exc:          # noqa: BLE001 - reported, not hidden
+            print(f"bench: mceik_comm unavailable ({exc}); gathering with torch.distributed", file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()) and comm is not None:
+            comm.close()
+            comm = None
+        gather_path = "mceik_mcmc_gather (RCCL)" if comm is not None else "torch.distributed gather (RCCL)"
         if rank == 0:
             post = torch.empty((per_gpu * world, p.ncell), dtype=torch.int32, device=dev)
             post_l = torch.empty(per_gpu * world, dtype=torch.float64, device=dev)
@@ -193,8 +208,13 @@ def main():
     t0 = time.perf_counter()
     smp.run(args.steps)
     # checkpoint: the kept posterior states of every chain -> rank 0 (RCCL over xGMI)
-    if world > 1:
+    if world > 1 and comm is not None:
         comm.gather(smp, per_gpu * world, which=1, root=0, v_out=post, logl_out=post_l if rank == 0 else None)
+    elif world > 1:
+        gv, gl = mcmc.gather_kept(smp, per_gpu * world, device=dev)
+        if rank == 0:
+            post.copy_(gv)
+            post_l.copy_(gl)
     else:
         smp.samples(max_states=1, device_ptr=post.data_ptr())
     torch.cuda.synchronize(dev)
@@ -212,7 +232,8 @@ def main():
         tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=dev)
         if rank == 0:
             gather_check = bool(torch.equal(tv, post) and torch.equal(tl, post_l))
-        comm.close()
+        if comm is not None:
+            comm.close()
     fsm_ms, nlaunch, iters, (bricks, segs, segs_changed) = smp.fsm_stats()
     _, logl, nacc, _ = smp.state()
     smp.close()
@@ -279,7 +300,7 @@ def main():
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
         if gather_check is not None:
-            line["gather"] = {"path": "mceik_mcmc_gather (RCCL)", "equals_torch_gather": gather_check}
+            line["gather"] = {"path": gather_path, "equals_torch_gather": gather_check}
         if args.raw_stats:
             line["fsm_raw"] = {"bricks": bricks, "segs": segs, "segs_changed": segs_changed, "iters": iters,
                                "launches": nlaunch}

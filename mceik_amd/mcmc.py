@@ -445,11 +445,14 @@ class Comm:
     def __init__(self, rank, world, device, bootstrap=None):
         L = _lib.lib()
         uid = (C.c_ubyte * 128)()
-        if rank == 0 and L.mceik_comm_unique_id(uid) != 0:
-            raise RuntimeError("mceik_comm_unique_id failed")
+        mine = None
+        if rank == 0 and L.mceik_comm_unique_id(uid) == 0:
+            mine = bytes(uid)
         if world > 1:
-            got = bootstrap(bytes(uid) if rank == 0 else None)
-            C.memmove(uid, got, 128)
+            mine = bootstrap(mine if rank == 0 else None)     # every rank learns the id, or that there is none
+        if mine is None:
+            raise RuntimeError("mceik_comm_unique_id failed on rank 0")
+        C.memmove(uid, mine, 128)
         h = C.c_void_p()
         if L.mceik_comm_init(uid, int(world), int(rank), int(device), C.byref(h)) != 0:
             raise RuntimeError("mceik_comm_init failed")
