@@ -22,5 +22,6 @@ fi
 timeout -k 10 200 python3 bench.py --config C2 --steps 3 --warmup 1 --no-cpu-baseline > "$O/bench_c2.log" 2>&1
 timeout -k 10 300 python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu-baseline > "$O/bench_c5.log" 2>&1
 timeout -k 10 300 python3 bench.py --precision 64 --steps 1 --warmup 1 --no-cpu-baseline > "$O/bench_c3_fp64.log" 2>&1
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
 timeout -k 10 400 python3 bench.py > "$O/bench_default.log" 2>&1
 echo done > "$O/DONE"
