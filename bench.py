@@ -139,6 +139,14 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    # MCEIK_BENCH_REHEARSAL=1: rehearse the N > 1 flow on ONE GPU (every rank on
+    # device 0, torch.distributed over gloo, host-side gather; RCCL takes one
+    # rank per GPU, so the library communicator is skipped).  A correctness
+    # drill of sharding, barriers, max-over-ranks timing and the gather; its
+    # throughput is not a scaling number.
+    rehearse = os.environ.get("MCEIK_BENCH_REHEARSAL") == "1"
+    if rehearse:
+        local_rank = 0
     from mceik_amd import mcmc
 
     cfg = mcmc.CONFIGS[args.config]
@@ -158,7 +166,11 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    red_dev = torch.device("cpu") if rehearse else dev      # where the small reductions live
     # picks from the GPU forward of the true model (replaces the analytic ones)
     tt = mcmc.picks_from_forward(local_rank)(p)
     rng = np.random.default_rng(p.seed + 1)
@@ -181,18 +193,20 @@ def main():
         # If the library cannot build its communicator on this node, every rank
         # uses torch.distributed's gather instead (same bytes, same collective)
         # and the line says so.
-        ok = 1
-        try:
-            comm = mcmc.Comm.from_torch(local_rank)
-        except Exception as exc:          # noqa: BLE001 - reported, not hidden
-            print(f"bench: mceik_comm unavailable ({exc}); gathering with torch.distributed", file=sys.stderr)
-            ok = 0
-        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        ok = 0 if rehearse else 1
+        if not rehearse:
+            try:
+                comm = mcmc.Comm.from_torch(local_rank)
+            except Exception as exc:          # noqa: BLE001 - reported, not hidden
+                print(f"bench: mceik_comm unavailable ({exc}); gathering with torch.distributed", file=sys.stderr)
+                ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=red_dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if not int(flag.item()) and comm is not None:
             comm.close()
             comm = None
-        gather_path = "mceik_mcmc_gather (RCCL)" if comm is not None else "torch.distributed gather (RCCL)"
+        gather_path = ("mceik_mcmc_gather (RCCL)" if comm is not None else
+                       "torch.distributed gather (gloo; one-GPU rehearsal)" if rehearse else "torch.distributed gather (RCCL)")
         if rank == 0:
             post = torch.empty((per_gpu * world, p.ncell), dtype=torch.int32, device=dev)
             post_l = torch.empty(per_gpu * world, dtype=torch.float64, device=dev)
@@ -211,7 +225,7 @@ def main():
     if world > 1 and comm is not None:
         comm.gather(smp, per_gpu * world, which=1, root=0, v_out=post, logl_out=post_l if rank == 0 else None)
     elif world > 1:
-        gv, gl = mcmc.gather_kept(smp, per_gpu * world, device=dev)
+        gv, gl = mcmc.gather_kept(smp, per_gpu * world, device=None if rehearse else dev)
         if rank == 0:
             post.copy_(gv)
             post_l.copy_(gl)
@@ -223,15 +237,15 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gather_check = None
     if world > 1:
         # outside the timed region: the library gather == torch.distributed's gather
-        tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=dev)
+        tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=None if rehearse else dev)
         if rank == 0:
-            gather_check = bool(torch.equal(tv, post) and torch.equal(tl, post_l))
+            gather_check = bool(torch.equal(tv.to(dev), post) and torch.equal(tl.to(dev), post_l))
         if comm is not None:
             comm.close()
     fsm_ms, nlaunch, iters, (bricks, segs, segs_changed) = smp.fsm_stats()
@@ -299,6 +313,8 @@ def main():
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
+        if rehearse:
+            line["rehearsal"] = "one GPU shared by all ranks (MCEIK_BENCH_REHEARSAL=1): not a scaling measurement"
         if gather_check is not None:
             line["gather"] = {"path": gather_path, "equals_torch_gather": gather_check}
         if args.raw_stats:
