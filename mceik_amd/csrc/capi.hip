@@ -20,6 +20,7 @@
 #include "fsm_single.h"
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st);
+hipError_t fsm_zero_words(unsigned *p, int n, hipStream_t st);
 int fsm_occupancy(const FsmLaunch &L, int is_double);
 size_t fsm_launch_lds_bytes(const FsmLaunch &L, int is_double);
 int fsm_launch_kind(const FsmLaunch &L, int is_double);
@@ -261,7 +262,7 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
     fill_launch(L, b);
     char *ws = (char *)workspace;
     L.counter = (unsigned *)(ws + w.counter);
-    HIPCHK(hipMemsetAsync(L.counter, 0, 1024, st));
+    HIPCHK(fsm_zero_words(L.counter, 256, st));          // 8 queue heads, 128 B apart (graph-safe)
     if (b->slow_mode == 0) {
         void *sb = ws + w.slow;
         if (is_double)

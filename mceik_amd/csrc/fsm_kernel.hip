@@ -1124,6 +1124,20 @@ size_t fsm_launch_lds_bytes(const FsmLaunch &L, int is_double)
 }
 int fsm_launch_kind(const FsmLaunch &L, int is_double) { return use_fsm16(L, is_double) ? 16 : 8; }
 
+// Zeroes the launch's work-queue heads with a kernel rather than
+// hipMemsetAsync: inside a captured HIP graph the memset node was not replayed
+// (ROCm 7.2; every replay after the first found the queues drained and ran no
+// solve, tests/test_gpu_fsm.py::test_batch_solve_captured_in_a_graph_bitwise).
+__global__ void fsm_zero_words_kernel(unsigned *p, int n)
+{
+    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0u;
+}
+hipError_t fsm_zero_words(unsigned *p, int n, hipStream_t st)
+{
+    hipLaunchKernelGGL(fsm_zero_words_kernel, dim3(1), dim3(256), 0, st, p, n);
+    return hipGetLastError();
+}
+
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st)
 {
     if (use_fsm16(L, is_double)) return fsm16_launch(L, nwaves, st);

@@ -380,3 +380,40 @@ def test_relocate_single_pass_c3_catalogue():
     b, tb = relocate(tables, events, log_pdf=True, single_pass=False)
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     assert torch.equal(ta.view(torch.int32), tb.view(torch.int32))
+
+
+def test_batch_solve_captured_in_a_graph_bitwise():
+    """mceik_fsm_batch_solve only enqueues work (no allocation, no host sync;
+    include/mceik_eikonal.h): captured once in a HIP graph (torch.cuda.graph)
+    and replayed on new slowness, its tables and iteration counts are bitwise
+    those of eager launches -- the sampler's 16-z cell-cache instance."""
+    dev = _dev()
+    from mceik_amd.eikonal import BatchSolver
+    n, h, nref, nm = 40, 100.0, (4, 4, 4), 3
+    nc = (n // 4) ** 3
+    rng = np.random.default_rng(21)
+    src = torch.tensor(np.stack([np.zeros(4), rng.uniform(200, 3700, 4), rng.uniform(200, 3700, 4),
+                                 np.full(4, 3900.0)], 1)[:, None, :])
+    ev = torch.tensor(rng.integers(0, n ** 3, 12).astype(np.int32))
+    src, ev = src.to(dev), ev.to(dev)                   # no host copies inside the capture
+    bs = BatchSolver(n, n, n, h, 0.0, 0.0, 0.0, 50, 1e-8, 32, nref=nref, fast_sqrt=True)
+    models = [torch.tensor((1.0 / rng.integers(2500, 6500, (nm, nc))).astype(np.float32), device=dev) for _ in range(3)]
+    eager = []
+    for m in models:
+        o = bs.solve(src, m, ev_node=ev)
+        torch.cuda.synchronize()
+        eager.append((o["ttab"].clone(), o["niter"].clone()))
+    slow = models[0].clone()
+    bs.solve(src, slow, ev_node=ev)                      # warm: workspace allocated outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            out = bs.solve(src, slow, ev_node=ev, stream=s.cuda_stream)
+    for m, (tt, it) in zip(models, eager):
+        slow.copy_(m)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out["ttab"].view(torch.int32), tt.view(torch.int32))
+        assert torch.equal(out["niter"], it)
