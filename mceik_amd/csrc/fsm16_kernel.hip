@@ -247,6 +247,14 @@ __device__ __forceinline__ void store16_plain(Rsrc r, uint32_t off, const float 
 }
 
 // ---- brick / halo addressing ------------------------------------------------
+#ifndef MCEIK_HALO_AUX
+#define MCEIK_HALO_AUX MCEIK_LD_AUX
+#endif
+__device__ __forceinline__ void bload4h(Rsrc r, uint32_t off, float (&v)[4])
+{
+    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MCEIK_HALO_AUX));
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
 struct BInfo16 {
     uint32_t seg;            // own 64-B segment (OOB if none)
     uint32_t zh;             // z-upwind node of a run start (prefetch only)
@@ -626,8 +634,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     {
         const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
-        bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hq[0]));
-        bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hq[4]));
+        bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hq[0]));
+        bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hq[4]));
         TRAF(S, 1, ho != OOB, 32);
     }
     zc = bload1(ur, b0.zh, 0.0f);
@@ -651,8 +659,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     {
         const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
-        bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
-        bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
+        bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
+        bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
         TRAF(S, 1, ho != OOB, 32);
     }
     zn = bload1(ur, b1.zh, 0.0f);
@@ -719,8 +727,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
         {
             const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
-            bload4(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
-            bload4(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
+            bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
+            bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
             TRAF(S, 1, ho != OOB, 32);
             TRAF(S, 0, b3.seg != OOB, 64);
             TRAF(S, 2, b3.zh != OOB, 4);

@@ -207,9 +207,12 @@ __device__ __forceinline__ void block_zcells(const FsmLaunch &L, int kb, int tz,
     ncz = (int)(((unsigned)b * L.magic_rz) >> 20) - cz0 + 1;
 }
 
+#ifndef MCEIK_LD_AUX
+#define MCEIK_LD_AUX 0
+#endif
 __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, float (&v)[4])
 {
-    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MCEIK_LD_AUX));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, double (&v)[4])
