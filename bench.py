@@ -173,6 +173,7 @@ def main():
     red_dev = torch.device("cpu") if rehearse else dev      # where the small reductions live
     # picks from the GPU forward of the true model (replaces the analytic ones)
     tt = mcmc.picks_from_forward(local_rank)(p)
+    torch.cuda.empty_cache()             # the forward's workspace: the sampler sizes its waves to HBM
     rng = np.random.default_rng(p.seed + 1)
     # pick noise sigma and varObs = sigma^2 at the scale one proposal moves a
     # travel time (~1 ms for 50 m/s on a 400-m cell), so the posterior is not

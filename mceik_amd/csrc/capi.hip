@@ -137,8 +137,8 @@ static int device_cus()
 }
 
 // Scratch budget for the per-wave u / u0 fields, fixed at the first call (so
-// workspace_bytes and batch_solve agree): MCEIK_FSM_WS_GB if set, else half of
-// the device's total memory (144 GB on a 288-GB MI355X).
+// workspace_bytes and batch_solve agree): MCEIK_FSM_WS_GB if set, else 80% of
+// the device's total memory (230 GB on a 288-GB MI355X).
 static size_t ws_budget_bytes()
 {
     static size_t budget = 0;
@@ -149,7 +149,8 @@ static size_t ws_budget_bytes()
             budget = (size_t)(gb * 1073741824.0);
         } else {
             size_t fr = 0, tot = 0;
-            budget = hipMemGetInfo(&fr, &tot) == hipSuccess && tot ? tot / 2 : (size_t)96 << 30;
+            // at 256^3 (128 MiB of u + u0 per wave): 6.7 waves/CU (half: 4.2)
+            budget = hipMemGetInfo(&fr, &tot) == hipSuccess && tot ? tot / 5 * 4 : (size_t)96 << 30;
         }
     }
     return budget;
