@@ -31,6 +31,7 @@ hipError_t fsm_to_brick_f32(const float *src, float *dst, const FsmLaunch &L, in
 hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st);
 hipError_t mcmc_init_loglik(const McmcDev &D, hipStream_t st);
 hipError_t mcmc_accept(const McmcDev &D, int keep_slot, hipStream_t st);
+hipError_t mcmc_lpt_order(const unsigned long long *clk, int nsolve, int *order, hipStream_t st);
 hipError_t l2_gridsearch_f32(int ldgrd, int ngrd, int nev, int iwantOT, float t0use, const int *ev_ptr,
                              const int *obs_row, const float *tc, const float *wt, const float *xnorm,
                              const float *test, float *t0, float *objfn, int negate, hipStream_t st);
@@ -973,6 +974,9 @@ struct mceik_mcmc {
     double fsm_ms;                     // folded kernel time (ms)
     unsigned long long *d_iters;
     int *d_ierr;
+    unsigned long long *d_clock;       // per-solve start/end stamps of the last launch (queue order, report)
+    int *d_order;                      // longest-first queue order for the next launch (MCEIK_LPT=1), or null
+    bool report;                       // MCEIK_SOLVE_CLOCK_REPORT=1
     mceik_fsm_batch fb;
     int device, max_samples, nburn, keepk, nkept, niter_total;
     int nkept_base;                    // nkept at the last restore: earlier states are not in the ring
@@ -1074,7 +1078,36 @@ static int mcmc_forward(mceik_mcmc *s, bool timed)
         HIPCHK(hipEventRecord(s->ev[2 * r + 1], s->stream));
         s->nlaunch++;
     }
+    if (s->d_order) {       // the next launch pulls this launch's longest solves first
+        HIPCHK(mcmc_lpt_order(s->d_clock, s->fb.nmodel * s->fb.nstat, s->d_order, s->stream));
+        s->fb.solve_order = s->d_order;
+    }
     return 0;
+}
+
+// MCEIK_SOLVE_CLOCK_REPORT=1: how busy the persistent waves were in the last
+// launch (sum of solve durations / (waves x launch span)); synchronises.
+static void clock_report(mceik_mcmc *s, const char *tag)
+{
+    const size_t n = (size_t)s->fb.nmodel * s->fb.nstat;
+    std::vector<unsigned long long> clk(n * 2);
+    if (hipStreamSynchronize(s->stream) != hipSuccess ||
+        hipMemcpy(clk.data(), s->d_clock, clk.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    double busy = 0.0, dmin = 1e30, dmax = 0.0;
+    for (size_t i = 0; i < clk.size(); i += 2) {
+        t0 = clk[i] < t0 ? clk[i] : t0;
+        t1 = clk[i + 1] > t1 ? clk[i + 1] : t1;
+        const double d = (double)(clk[i + 1] - clk[i]);
+        busy += d;
+        dmin = d < dmin ? d : dmin;
+        dmax = d > dmax ? d : dmax;
+    }
+    const int nw = ws_layout(&s->fb).nwaves;
+    fprintf(stderr, "mceik solve clock (%s, %s order): %zu solves on %d waves, launch %.1f ms, solve %.1f..%.1f ms "
+                    "(mean %.1f), waves busy %.2f%%\n", tag, s->d_order ? "longest-first" : "id", n, nw,
+            (t1 - t0) * 1e-5, dmin * 1e-5, dmax * 1e-5, busy / n * 1e-5, 100.0 * busy / ((double)nw * (double)(t1 - t0)));
 }
 
 // After a forward: every solve's reference ierr must be 0 (a station on the
@@ -1237,45 +1270,38 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         mceik_mcmc_finalize(&s);
         return -1;
     }
-    // initial log-likelihood of every chain.  MCEIK_SOLVE_CLOCK_REPORT=1: time
-    // every solve of this launch and print how busy the persistent waves were
-    // (diagnostic for the work-queue tail)
-    unsigned long long *d_clock = nullptr;
+    // initial log-likelihood of every chain.  Every launch stamps its solves
+    // (solve_clock) and with MCEIK_LPT=1 the next launch drains each queue
+    // longest solve first (mcmc_lpt_order; the init forward runs in id order).
+    // Off by default: at C3 the waves are 96.6% busy in id order and longest-
+    // first made the mean solve 4% slower.
+    // MCEIK_SOLVE_CLOCK_REPORT=1: print how busy the persistent waves were
+    // (init forward; diagnostic for the work-queue tail)
+    const char *lpt_env = getenv("MCEIK_LPT");
+    const bool lpt = lpt_env && lpt_env[0] == '1';
     const char *rep_env = getenv("MCEIK_SOLVE_CLOCK_REPORT");
     const bool report = rep_env && rep_env[0] == '1';
-    if (report && dalloc(s, &d_clock, (size_t)nch * nstat * 2)) {
+    if ((lpt || report) && dalloc(s, &s->d_clock, (size_t)nch * nstat * 2)) {
         mceik_mcmc_finalize(&s);
         return -1;
     }
+    if (lpt && dalloc(s, &s->d_order, (size_t)nch * nstat)) {
+        mceik_mcmc_finalize(&s);
+        return -1;
+    }
+    unsigned long long *d_clock = s->d_clock;
     b.solve_clock = d_clock;
+    b.solve_order = nullptr;
     if (mcmc_forward(s, false) || mcmc_init_loglik(D, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
         mceik_mcmc_finalize(&s);
         return -1;
     }
-    b.solve_clock = nullptr;
     if (check_forward_ierr(s, "mceik_mcmc_init")) {
         mceik_mcmc_finalize(&s);
         return 2;
     }
-    if (report) {
-        std::vector<unsigned long long> clk((size_t)nch * nstat * 2);
-        if (hipMemcpy(clk.data(), d_clock, clk.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-            unsigned long long t0 = ~0ull, t1 = 0;
-            double busy = 0.0, dmin = 1e30, dmax = 0.0;
-            for (size_t i = 0; i < clk.size(); i += 2) {
-                t0 = clk[i] < t0 ? clk[i] : t0;
-                t1 = clk[i + 1] > t1 ? clk[i + 1] : t1;
-                const double d = (double)(clk[i + 1] - clk[i]);
-                busy += d;
-                dmin = d < dmin ? d : dmin;
-                dmax = d > dmax ? d : dmax;
-            }
-            const int nw = ws_layout(&b).nwaves;
-            fprintf(stderr, "mceik solve clock: %d solves on %d waves, launch %.1f ms, solve %.1f..%.1f ms "
-                            "(mean %.1f), waves busy %.2f%%\n", nch * nstat, nw, (t1 - t0) * 1e-5, dmin * 1e-5,
-                    dmax * 1e-5, busy / (nch * nstat) * 1e-5, 100.0 * busy / ((double)nw * (double)(t1 - t0)));
-        }
-    }
+    s->report = report;
+    if (report) clock_report(s, "init");
     hipMemset(s->d_iters, 0, (4 + MCEIK_TRAFFIC_N) * sizeof(unsigned long long));
     *out = s;
     return 0;
@@ -1300,6 +1326,7 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
         uint64_t step = (uint64_t)s->step;
         HIPCHK(mcmc_propose(s->D, step, s->stream));
         if (mcmc_forward(s, true)) return -1;
+        if (s->report) clock_report(s, "step");
         int slot = -1;
         if (s->max_samples && s->step >= s->nburn && (s->step - s->nburn) % s->keepk == 0) {
             slot = s->nkept % s->max_samples;

@@ -326,6 +326,50 @@ hipError_t gridsearch_f90(int is_double, int ldgrd, int ngrd, int nuse, int iwan
     return hipGetLastError();
 }
 
+// Longest-first queue order for the next FSM launch.  The persistent waves
+// pull solves from 8 queues (fsm_device.h next_solve: group g drains slots
+// [nsolve*g/8, nsolve*(g+1)/8) and then steals); a chain's proposal changes
+// one cell, so a solve costs about what it cost last step.  Each group's
+// solves are ranked by last launch's duration (s_memrealtime stamps, the
+// kernel's solve_clock), longest first, ties by solve id, and written to
+// the group's own slots: the set of solves per group -- hence per XCD -- is
+// unchanged, only the order within it.  Results do not depend on the order.
+// Rank by counting over the group's keys staged through LDS (n^2 / group:
+// 4096-solve groups at C3 take well under a millisecond).
+#define LPT_TILE 2048
+__global__ __launch_bounds__(256) void lpt_order_kernel(const unsigned long long *clk, int nsolve, int *order)
+{
+    __shared__ unsigned key[LPT_TILE];
+    const int g = blockIdx.y;
+    const int lo = (int)((long long)nsolve * g / 8), hi = (int)((long long)nsolve * (g + 1) / 8), n = hi - lo;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if ((int)blockIdx.x * 256 >= n) return;                 // uniform per block
+    auto dur = [&](int j) -> unsigned {
+        const unsigned long long d = clk[2 * (size_t)j + 1] - clk[2 * (size_t)j];
+        return d > 0xffffffffull ? 0xffffffffu : (unsigned)d;
+    };
+    const unsigned ki = i < n ? dur(lo + i) : 0u;
+    int rank = 0;
+    for (int t0 = 0; t0 < n; t0 += LPT_TILE) {
+        const int m = min(LPT_TILE, n - t0);
+        __syncthreads();
+        for (int j = threadIdx.x; j < m; j += 256) key[j] = dur(lo + t0 + j);
+        __syncthreads();
+        for (int j = 0; j < m; j++) {
+            const unsigned kj = key[j];
+            rank += (kj > ki) || (kj == ki && t0 + j < i);
+        }
+    }
+    if (i < n) order[lo + rank] = lo + i;
+}
+
+hipError_t mcmc_lpt_order(const unsigned long long *clk, int nsolve, int *order, hipStream_t st)
+{
+    const int nmax = (nsolve + 7) / 8;
+    hipLaunchKernelGGL(lpt_order_kernel, dim3((nmax + 255) / 256, 8), dim3(256), 0, st, clk, nsolve, order);
+    return hipGetLastError();
+}
+
 hipError_t mcmc_propose(const McmcDev &D, uint64_t step, hipStream_t st)
 {
     hipLaunchKernelGGL(propose_kernel, dim3((D.nchains + 255) / 256), dim3(256), 0, st, D, step);
