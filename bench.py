@@ -4,7 +4,9 @@
 One step = one proposal for every chain on every GPU: propose (one inversion
 cell per chain) -> batched FSM solves (chains x stations, HIP, fp32) ->
 travel times at the events -> L2 misfit with analytic origin time ->
-Metropolis.  N=1 runs configs[2] ("C3": 1024 chains, 128^3, 32 stations);
+Metropolis (the sampler runs its chains as two halves on two streams, the
+library default; --pipes 1 for one launch per step).  N=1 runs configs[2]
+("C3": 1024 chains, 128^3, 32 stations);
 --gpus N keeps 1024 chains per GPU (weak scaling; N=8 is configs[3], 8192
 chains) and gathers the kept posterior states to rank 0 over RCCL at the
 end of the timed region (the checkpoint).
@@ -134,7 +136,11 @@ def main():
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64),
                     help="FSM arithmetic (64: the reference's literal fp64 update; tables fp32 either way)")
+    ap.add_argument("--pipes", type=int, default=2, choices=(1, 2),
+                    help="the sampler's chains as two halves on two streams (the library default, DESIGN.md "
+                         "s.3.5) or one launch per step (1)")
     args = ap.parse_args()
+    os.environ["MCEIK_PIPES"] = str(args.pipes)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -274,7 +280,14 @@ def main():
         alg_bytes = bricks * (n_nodes / nbricks) * bpn    # this rank's launches
         full_bytes = iters * 8.0 * n_nodes * bpn          # the same iterations without skipping
         avg_ms = fsm_ms / max(nlaunch, 1)
-        achieved = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
+        achieved = per_launch = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
+        pipes = round(nlaunch / max(args.steps, 1))       # 1 if the sampler fell back to one pipe
+        if pipes == 2:
+            # two half launches per step, overlapped: a half's HIP-event span also
+            # covers the time it waits for the other half's waves, so price one
+            # step's algorithmic bytes on the step's wall time instead (includes
+            # propose/accept and the gather: conservative)
+            achieved = alg_bytes / elapsed / 1e9                  # this rank's bytes, the timed region
         traffic = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tf):
@@ -300,13 +313,19 @@ def main():
             "config": {"workload": f"{args.config}: {per_gpu} chains/GPU, {p.nx}^3 grid, {p.nstat} stations, "
                                    f"{p.nevents} events, nref=4",
                        "chains_per_gpu": per_gpu, "chains_total": per_gpu * world, "grid": [p.nx, p.ny, p.nz],
-                       "stations": p.nstat, "events": p.nevents, "parallelism": f"chains sharded over {world} GPU(s)"},
+                       "stations": p.nstat, "events": p.nevents, "parallelism": f"chains sharded over {world} GPU(s)",
+                       "pipes": pipes},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kname,
                          "kernel_rev": KERNEL_REV,
+                         "timing": ("wall time per step (two overlapped half launches, MCEIK_PIPES=2)"
+                                    if pipes == 2 else "HIP events around each FSM launch"),
+                         "traffic_per": "step (= one single-pipe launch, profiles/traffic.json)",
                          "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
                          "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),
+                         "launches_per_step": round(nlaunch / max(args.steps, 1), 3),
+                         "frac_per_launch_events": round(per_launch / HBM_PEAK_GBS, 4),
                          "iterations_per_solve": round(iters / max(nlaunch, 1) / (per_gpu * p.nstat), 3),
                          "brick_visit_fraction": round(bricks / max(1.0, iters * 8.0 * nbricks), 4),
                          "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),

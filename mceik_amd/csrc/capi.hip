@@ -977,6 +977,18 @@ struct mceik_mcmc {
     unsigned long long *d_clock;       // per-solve start/end stamps of the last launch (queue order, report)
     int *d_order;                      // longest-first queue order for the next launch (MCEIK_LPT=1), or null
     bool report;                       // MCEIK_SOLVE_CLOCK_REPORT=1
+    // Two pipes (default; MCEIK_PIPES=1 turns them off): the chains run as two
+    // halves on two streams of their own, each half's next FSM launch queued
+    // behind its own accept, so one half's launch fills the waves the other
+    // half's queue tail leaves idle.  Results are those of
+    // one pipe bit for bit.
+    int npipe;
+    hipStream_t pst[2];
+    hipEvent_t pfork, pjoin[2];
+    McmcDev pD[2];
+    mceik_fsm_batch pfb[2];
+    void *pws1;                        // pipe 1's workspace (pipe 0 uses ws)
+    size_t pws1_bytes;
     mceik_fsm_batch fb;
     int device, max_samples, nburn, keepk, nkept, niter_total;
     int nkept_base;                    // nkept at the last restore: earlier states are not in the ring
@@ -1056,8 +1068,12 @@ static int fold_launch(mceik_mcmc *s, long long k)
     return 0;
 }
 
-static int mcmc_forward(mceik_mcmc *s, bool timed)
+static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
 {
+    mceik_fsm_batch &fb = pipe < 0 ? s->fb : s->pfb[pipe];
+    void *ws = pipe == 1 ? s->pws1 : s->ws;
+    const size_t ws_bytes = pipe == 1 ? s->pws1_bytes : s->ws_bytes;
+    const hipStream_t st = pipe < 0 ? s->stream : s->pst[pipe];
     int r = 0;
     if (timed) {
         // the ring slot of launch nlaunch - RING is reused: fold that launch first
@@ -1071,14 +1087,14 @@ static int mcmc_forward(mceik_mcmc *s, bool timed)
             HIPCHK(hipEventCreate(&s->ev[2 * s->ev_made + 1]));
             s->ev_made++;
         }
-        HIPCHK(hipEventRecord(s->ev[2 * r], s->stream));
+        HIPCHK(hipEventRecord(s->ev[2 * r], st));
     }
-    if (mceik_fsm_batch_solve(&s->fb, s->ws, s->ws_bytes, s->stream)) return -1;
+    if (mceik_fsm_batch_solve(&fb, ws, ws_bytes, st)) return -1;
     if (timed) {
-        HIPCHK(hipEventRecord(s->ev[2 * r + 1], s->stream));
+        HIPCHK(hipEventRecord(s->ev[2 * r + 1], st));
         s->nlaunch++;
     }
-    if (s->d_order) {       // the next launch pulls this launch's longest solves first
+    if (s->d_order && pipe < 0) {       // the next launch pulls this launch's longest solves first
         HIPCHK(mcmc_lpt_order(s->d_clock, s->fb.nmodel * s->fb.nstat, s->d_order, s->stream));
         s->fb.solve_order = s->d_order;
     }
@@ -1091,7 +1107,7 @@ static void clock_report(mceik_mcmc *s, const char *tag)
 {
     const size_t n = (size_t)s->fb.nmodel * s->fb.nstat;
     std::vector<unsigned long long> clk(n * 2);
-    if (hipStreamSynchronize(s->stream) != hipSuccess ||
+    if ((s->npipe > 1 ? hipDeviceSynchronize() : hipStreamSynchronize(s->stream)) != hipSuccess ||
         hipMemcpy(clk.data(), s->d_clock, clk.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
         return;
     unsigned long long t0 = ~0ull, t1 = 0;
@@ -1108,6 +1124,63 @@ static void clock_report(mceik_mcmc *s, const char *tag)
     fprintf(stderr, "mceik solve clock (%s, %s order): %zu solves on %d waves, launch %.1f ms, solve %.1f..%.1f ms "
                     "(mean %.1f), waves busy %.2f%%\n", tag, s->d_order ? "longest-first" : "id", n, nw,
             (t1 - t0) * 1e-5, dmin * 1e-5, dmax * 1e-5, busy / n * 1e-5, 100.0 * busy / ((double)nw * (double)(t1 - t0)));
+}
+
+// A view of chains [off, off + n) of the sampler's device state / batch.
+static McmcDev dev_view(const McmcDev &D, int off, int n)
+{
+    McmcDev V = D;
+    const size_t o = (size_t)off, oc = o * D.ncell;
+    V.nchains = n;
+    V.chain_offset = D.chain_offset + off;
+    V.v += oc; V.slow_cur += oc; V.slow_prop += oc;
+    V.logl += o; V.naccept += o;
+    V.prop_cell += o; V.prop_v += o; V.prop_inprior += o; V.prop_logu += o; V.accept += o;
+    V.ttab += o * D.nstat * D.nev;
+    if (V.keep_v) V.keep_v += oc;
+    if (V.keep_logl) V.keep_logl += o;
+    return V;
+}
+
+static mceik_fsm_batch batch_view(const mceik_fsm_batch &b, int off, int n, size_t ncell)
+{
+    mceik_fsm_batch V = b;
+    const size_t o = (size_t)off, os = o * b.nstat;
+    V.nmodel = n;
+    V.slow = (const float *)b.slow + o * ncell;
+    V.ttab = b.ttab + os * b.nev;
+    V.niter = b.niter + os;
+    V.ierr = b.ierr + os;
+    V.solve_order = nullptr;
+    V.solve_clock = b.solve_clock ? b.solve_clock + 2 * os : nullptr;
+    return V;
+}
+
+// Two pipes: halves of the chains, their own streams and a second workspace.  Returns nonzero on a HIP failure; falls back to one pipe
+// (with a message) when the second workspace does not fit.
+static int pipes_setup(mceik_mcmc *s)
+{
+    const int nch = s->D.nchains, n0 = nch / 2;
+    const size_t ncell = (size_t)s->D.ncell;
+    s->pD[0] = dev_view(s->D, 0, n0);
+    s->pD[1] = dev_view(s->D, n0, nch - n0);
+    s->pfb[0] = batch_view(s->fb, 0, n0, ncell);
+    s->pfb[1] = batch_view(s->fb, n0, nch - n0, ncell);
+    s->pws1_bytes = mceik_fsm_workspace_bytes(&s->pfb[1]);
+    if (mceik_fsm_workspace_bytes(&s->pfb[0]) > s->ws_bytes || hipMalloc(&s->pws1, s->pws1_bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        s->pws1 = nullptr;
+        fprintf(stderr, "mceik_mcmc_init: two pipes need a second %zu-B FSM workspace; running one pipe\n",
+                s->pws1_bytes);
+        return 0;
+    }
+    for (int k = 0; k < 2; k++) {
+        HIPCHK(hipStreamCreateWithFlags(&s->pst[k], hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&s->pjoin[k], hipEventDisableTiming));
+    }
+    HIPCHK(hipEventCreateWithFlags(&s->pfork, hipEventDisableTiming));
+    s->npipe = 2;
+    return 0;
 }
 
 // After a forward: every solve's reference ierr must be 0 (a station on the
@@ -1177,6 +1250,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     McmcDev &D = s->D;
     memset(&D, 0, sizeof(D));
     D.nchains = nch; D.chain_offset = o->chain_offset; D.ncell = ncell; D.nstat = nstat; D.nev = nev;
+    D.keep_stride = nch;
     D.vmin = o->vmin; D.vmax = o->vmax; D.dvmax = o->dvmax; D.seed = o->seed;
     // host-side problem tables
     std::vector<double> src((size_t)nstat * 4);
@@ -1302,6 +1376,12 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     }
     s->report = report;
     if (report) clock_report(s, "init");
+    s->npipe = 1;
+    const char *pipe_env = getenv("MCEIK_PIPES");       // default 2; MCEIK_PIPES=1: one pipe
+    if (!(pipe_env && atoi(pipe_env) == 1) && nch >= 2 && pipes_setup(s)) {
+        mceik_mcmc_finalize(&s);
+        return -1;
+    }
     hipMemset(s->d_iters, 0, (4 + MCEIK_TRAFFIC_N) * sizeof(unsigned long long));
     *out = s;
     return 0;
@@ -1322,18 +1402,37 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
         nsteps = left > 0 ? (int)left : 0;
     }
     DeviceScope dg(s->device);
+    const int np = s->npipe;
+    if (np > 1) {                       // both pipes start after the caller's stream
+        HIPCHK(hipEventRecord(s->pfork, s->stream));
+        for (int k = 0; k < np; k++) HIPCHK(hipStreamWaitEvent(s->pst[k], s->pfork, 0));
+    }
     for (int i = 0; i < nsteps; i++) {
         uint64_t step = (uint64_t)s->step;
-        HIPCHK(mcmc_propose(s->D, step, s->stream));
-        if (mcmc_forward(s, true)) return -1;
-        if (s->report) clock_report(s, "step");
         int slot = -1;
         if (s->max_samples && s->step >= s->nburn && (s->step - s->nburn) % s->keepk == 0) {
             slot = s->nkept % s->max_samples;
             s->nkept++;
         }
-        HIPCHK(mcmc_accept(s->D, slot, s->stream));
+        if (np > 1) {
+            for (int k = 0; k < np; k++) {
+                HIPCHK(mcmc_propose(s->pD[k], step, s->pst[k]));
+                if (mcmc_forward(s, true, k)) return -1;
+                HIPCHK(mcmc_accept(s->pD[k], slot, s->pst[k]));
+            }
+        } else {
+            HIPCHK(mcmc_propose(s->D, step, s->stream));
+            if (mcmc_forward(s, true)) return -1;
+            HIPCHK(mcmc_accept(s->D, slot, s->stream));
+        }
+        if (s->report) clock_report(s, "step");
         s->step++;
+    }
+    if (np > 1) {                       // the caller's stream continues after both
+        for (int k = 0; k < np; k++) {
+            HIPCHK(hipEventRecord(s->pjoin[k], s->pst[k]));
+            HIPCHK(hipStreamWaitEvent(s->stream, s->pjoin[k], 0));
+        }
     }
     return 0;
 }
@@ -1505,6 +1604,15 @@ extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
     mceik_mcmc *s = *ps;
     DeviceScope dg(s->device);
     hipStreamSynchronize(s->stream);
+    if (s->npipe > 1) {
+        for (int k = 0; k < 2; k++) {
+            hipStreamSynchronize(s->pst[k]);
+            hipStreamDestroy(s->pst[k]);
+            hipEventDestroy(s->pjoin[k]);
+        }
+        hipEventDestroy(s->pfork);
+    }
+    if (s->pws1) hipFree(s->pws1);
     for (void *p : s->allocs) hipFree(p);
     for (int i = 0; i < 2 * s->ev_made; i++) hipEventDestroy(s->ev[i]);
     if (s->ws) hipFree(s->ws);

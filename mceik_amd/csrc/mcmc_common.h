@@ -17,8 +17,9 @@ struct McmcDev {
     const float *ttab;             // [nchains][nstat][nev]
     const int *obs_ptr, *obs_stat, *obs_mask;
     const double *tobs, *tcorr, *var;
-    int *keep_v;                   // [max_samples][nchains][ncell]
-    double *keep_logl;             // [max_samples][nchains]
+    int *keep_v;                   // [max_samples][keep_stride][ncell]
+    double *keep_logl;             // [max_samples][keep_stride]
+    int keep_stride;               // chains per kept slot: the sampler's nchains (a pipe's view covers a part)
 };
 
 // One rank's chain shard as the checkpoint gather sees it (capi.hip

@@ -119,14 +119,14 @@ __global__ void accept_kernel(McmcDev D, int keep_slot)
         }
     }
     D.accept[c] = (unsigned char)acc;
-    if (keep_slot >= 0) D.keep_logl[(size_t)keep_slot * D.nchains + c] = D.logl[c];
+    if (keep_slot >= 0) D.keep_logl[(size_t)keep_slot * D.keep_stride + c] = D.logl[c];
 }
 
 // Kept state copy: [slot][chain][cell] int (after accept_kernel).
 __global__ void keep_kernel(McmcDev D, int keep_slot)
 {
     size_t n = (size_t)D.nchains * D.ncell;
-    int *dst = D.keep_v + (size_t)keep_slot * n;
+    int *dst = D.keep_v + (size_t)keep_slot * D.keep_stride * D.ncell;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = D.v[i];
 }

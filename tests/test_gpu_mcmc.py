@@ -218,3 +218,38 @@ def test_station_on_first_node_fails_init():
     p.sx[1] = p.x0
     with pytest.raises(RuntimeError):
         mcmc.Sampler(p, nchains=1)
+
+
+
+@pytest.mark.parametrize("nch,pipes", [(5, "2"), (8, "2"), (5, "1")], ids=["odd_halves", "even_halves", "one_pipe"])
+def test_pipes_bitwise(nch, pipes, monkeypatch):
+    """Two pipes (the default: halves of the chains on two streams, DESIGN.md
+    s.3.5) and one pipe (MCEIK_PIPES=1): models, logL, accept counts and kept
+    samples bit-identical to oracle_mcmc_run, with run() split over calls."""
+    _dev()
+    from mceik_amd import mcmc
+    monkeypatch.setenv("MCEIK_PIPES", pipes)
+    p = _problem(n=40, seed=9)
+    p.nburn, p.keepk = 1, 2                   # kept after steps 2, 4, 6
+    off = 3
+    s = mcmc.Sampler(p, nchains=nch, chain_offset=off, max_samples=8)
+    v0, logl0, _, _ = s.state()
+    s.run(2)
+    s.run(1)
+    s.run(3)
+    _, _, last_acc = s.last()
+    v, logl, nacc, step = s.state()
+    kv, kl = s.samples()
+    s.close()
+    P = O.make_problem(p)
+    vo, lo, acc, trace = O.mcmc_run(P, v0, logl0, off, 0, 6)
+    assert step == 6
+    assert np.array_equal(v, vo)
+    assert np.array_equal(logl.view(np.uint64), lo.view(np.uint64))
+    assert np.array_equal(last_acc, acc[-1])
+    assert nacc.sum() == acc.sum() and 0 < acc.sum() < acc.size
+    assert len(kv) == 3
+    for k, n in enumerate((2, 4, 6)):
+        vk, lk, _, _ = O.mcmc_run(P, v0, logl0, off, 0, n)
+        assert np.array_equal(kv[k], vk)
+        assert np.array_equal(kl[k].view(np.uint64), lk.view(np.uint64))
