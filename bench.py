@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64),
                     help="FSM arithmetic (64: the reference's literal fp64 update; tables fp32 either way)")
-    ap.add_argument("--pipes", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--pipes", type=int, default=2, choices=(1, 2, 3, 4),
                     help="the sampler's chains as two halves on two streams (the library default, DESIGN.md "
                          "s.3.5) or one launch per step (1)")
     args = ap.parse_args()
@@ -282,7 +282,7 @@ def main():
         avg_ms = fsm_ms / max(nlaunch, 1)
         achieved = per_launch = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
         pipes = round(nlaunch / max(args.steps, 1))       # 1 if the sampler fell back to one pipe
-        if pipes == 2:
+        if pipes > 1:
             # two half launches per step, overlapped: a half's HIP-event span also
             # covers the time it waits for the other half's waves, so price one
             # step's algorithmic bytes on the step's wall time instead (includes
@@ -319,8 +319,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kname,
                          "kernel_rev": KERNEL_REV,
-                         "timing": ("wall time per step (two overlapped half launches, MCEIK_PIPES=2)"
-                                    if pipes == 2 else "HIP events around each FSM launch"),
+                         "timing": (f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
+                                    if pipes > 1 else "HIP events around each FSM launch"),
                          "traffic_per": "step (= one single-pipe launch, profiles/traffic.json)",
                          "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
                          "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),

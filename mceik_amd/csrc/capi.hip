@@ -964,6 +964,7 @@ extern "C" int mceik_relocate(const mceik_relocate_batch *b, void *stream)
 // ---------------------------------------------------------------------------
 // MCMC sampler (include/mceik.h)
 #define MCEIK_EV_RING 32           // hipEvent pairs around timed FSM launches (fixed ring)
+#define MCEIK_MAX_PIPES 4
 
 struct mceik_mcmc {
     McmcDev D;
@@ -983,12 +984,12 @@ struct mceik_mcmc {
     // half's queue tail leaves idle.  Results are those of
     // one pipe bit for bit.
     int npipe;
-    hipStream_t pst[2];
-    hipEvent_t pfork, pjoin[2];
-    McmcDev pD[2];
-    mceik_fsm_batch pfb[2];
-    void *pws1;                        // pipe 1's workspace (pipe 0 uses ws)
-    size_t pws1_bytes;
+    hipStream_t pst[MCEIK_MAX_PIPES];
+    hipEvent_t pfork, pjoin[MCEIK_MAX_PIPES];
+    McmcDev pD[MCEIK_MAX_PIPES];
+    mceik_fsm_batch pfb[MCEIK_MAX_PIPES];
+    void *pws[MCEIK_MAX_PIPES];        // pipe k's workspace (pipe 0 uses ws)
+    size_t pws_bytes[MCEIK_MAX_PIPES];
     mceik_fsm_batch fb;
     int device, max_samples, nburn, keepk, nkept, niter_total;
     int nkept_base;                    // nkept at the last restore: earlier states are not in the ring
@@ -1071,8 +1072,8 @@ static int fold_launch(mceik_mcmc *s, long long k)
 static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
 {
     mceik_fsm_batch &fb = pipe < 0 ? s->fb : s->pfb[pipe];
-    void *ws = pipe == 1 ? s->pws1 : s->ws;
-    const size_t ws_bytes = pipe == 1 ? s->pws1_bytes : s->ws_bytes;
+    void *ws = pipe > 0 ? s->pws[pipe] : s->ws;
+    const size_t ws_bytes = pipe > 0 ? s->pws_bytes[pipe] : s->ws_bytes;
     const hipStream_t st = pipe < 0 ? s->stream : s->pst[pipe];
     int r = 0;
     if (timed) {
@@ -1156,30 +1157,40 @@ static mceik_fsm_batch batch_view(const mceik_fsm_batch &b, int off, int n, size
     return V;
 }
 
-// Two pipes: halves of the chains, their own streams and a second workspace.  Returns nonzero on a HIP failure; falls back to one pipe
-// (with a message) when the second workspace does not fit.
-static int pipes_setup(mceik_mcmc *s)
+// np pipes: parts of the chains, their own streams and workspaces (pipe 0
+// reuses the sampler's).  Returns nonzero on a HIP failure; falls back to one
+// pipe (with a message) when the extra workspaces do not fit.
+static int pipes_setup(mceik_mcmc *s, int np)
 {
-    const int nch = s->D.nchains, n0 = nch / 2;
+    const int nch = s->D.nchains;
     const size_t ncell = (size_t)s->D.ncell;
-    s->pD[0] = dev_view(s->D, 0, n0);
-    s->pD[1] = dev_view(s->D, n0, nch - n0);
-    s->pfb[0] = batch_view(s->fb, 0, n0, ncell);
-    s->pfb[1] = batch_view(s->fb, n0, nch - n0, ncell);
-    s->pws1_bytes = mceik_fsm_workspace_bytes(&s->pfb[1]);
-    if (mceik_fsm_workspace_bytes(&s->pfb[0]) > s->ws_bytes || hipMalloc(&s->pws1, s->pws1_bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        s->pws1 = nullptr;
-        fprintf(stderr, "mceik_mcmc_init: two pipes need a second %zu-B FSM workspace; running one pipe\n",
-                s->pws1_bytes);
+    for (int k = 0; k < np; k++) {
+        const int lo = (int)((long long)nch * k / np), hi = (int)((long long)nch * (k + 1) / np);
+        s->pD[k] = dev_view(s->D, lo, hi - lo);
+        s->pfb[k] = batch_view(s->fb, lo, hi - lo, ncell);
+    }
+    bool fit = mceik_fsm_workspace_bytes(&s->pfb[0]) <= s->ws_bytes;
+    size_t extra = 0;
+    for (int k = 1; k < np && fit; k++) {
+        s->pws_bytes[k] = mceik_fsm_workspace_bytes(&s->pfb[k]);
+        extra += s->pws_bytes[k];
+        if (hipMalloc(&s->pws[k], s->pws_bytes[k]) != hipSuccess) {
+            (void)hipGetLastError();
+            s->pws[k] = nullptr;
+            fit = false;
+        }
+    }
+    if (!fit) {
+        for (int k = 1; k < np; k++) if (s->pws[k]) { hipFree(s->pws[k]); s->pws[k] = nullptr; }
+        fprintf(stderr, "mceik_mcmc_init: %d pipes need %zu B more FSM workspace; running one pipe\n", np, extra);
         return 0;
     }
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < np; k++) {
         HIPCHK(hipStreamCreateWithFlags(&s->pst[k], hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&s->pjoin[k], hipEventDisableTiming));
     }
     HIPCHK(hipEventCreateWithFlags(&s->pfork, hipEventDisableTiming));
-    s->npipe = 2;
+    s->npipe = np;
     return 0;
 }
 
@@ -1378,7 +1389,10 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     if (report) clock_report(s, "init");
     s->npipe = 1;
     const char *pipe_env = getenv("MCEIK_PIPES");       // default 2; MCEIK_PIPES=1: one pipe
-    if (!(pipe_env && atoi(pipe_env) == 1) && nch >= 2 && pipes_setup(s)) {
+    int np = pipe_env ? atoi(pipe_env) : 2;
+    np = np < 1 ? 1 : np > MCEIK_MAX_PIPES ? MCEIK_MAX_PIPES : np;
+    if (np > nch) np = nch;
+    if (np > 1 && pipes_setup(s, np)) {
         mceik_mcmc_finalize(&s);
         return -1;
     }
@@ -1605,14 +1619,14 @@ extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
     DeviceScope dg(s->device);
     hipStreamSynchronize(s->stream);
     if (s->npipe > 1) {
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < s->npipe; k++) {
             hipStreamSynchronize(s->pst[k]);
             hipStreamDestroy(s->pst[k]);
             hipEventDestroy(s->pjoin[k]);
         }
         hipEventDestroy(s->pfork);
     }
-    if (s->pws1) hipFree(s->pws1);
+    for (int k = 1; k < MCEIK_MAX_PIPES; k++) if (s->pws[k]) hipFree(s->pws[k]);
     for (void *p : s->allocs) hipFree(p);
     for (int i = 0; i < 2 * s->ev_made; i++) hipEventDestroy(s->ev[i]);
     if (s->ws) hipFree(s->ws);

@@ -221,7 +221,7 @@ def test_station_on_first_node_fails_init():
 
 
 
-@pytest.mark.parametrize("nch,pipes", [(5, "2"), (8, "2"), (5, "1")], ids=["odd_halves", "even_halves", "one_pipe"])
+@pytest.mark.parametrize("nch,pipes", [(5, "2"), (8, "2"), (5, "1"), (7, "3")], ids=["odd_halves", "even_halves", "one_pipe", "three_pipes"])
 def test_pipes_bitwise(nch, pipes, monkeypatch):
     """Two pipes (the default: halves of the chains on two streams, DESIGN.md
     s.3.5) and one pipe (MCEIK_PIPES=1): models, logL, accept counts and kept
