@@ -1185,12 +1185,12 @@ static int pipes_setup(mceik_mcmc *s, int np)
         fprintf(stderr, "mceik_mcmc_init: %d pipes need %zu B more FSM workspace; running one pipe\n", np, extra);
         return 0;
     }
+    s->npipe = np;                     // finalize releases whatever was created
     for (int k = 0; k < np; k++) {
         HIPCHK(hipStreamCreateWithFlags(&s->pst[k], hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&s->pjoin[k], hipEventDisableTiming));
     }
     HIPCHK(hipEventCreateWithFlags(&s->pfork, hipEventDisableTiming));
-    s->npipe = np;
     return 0;
 }
 
@@ -1618,14 +1618,14 @@ extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
     mceik_mcmc *s = *ps;
     DeviceScope dg(s->device);
     hipStreamSynchronize(s->stream);
-    if (s->npipe > 1) {
-        for (int k = 0; k < s->npipe; k++) {
+    for (int k = 0; k < MCEIK_MAX_PIPES; k++) {
+        if (s->pst[k]) {
             hipStreamSynchronize(s->pst[k]);
             hipStreamDestroy(s->pst[k]);
-            hipEventDestroy(s->pjoin[k]);
         }
-        hipEventDestroy(s->pfork);
+        if (s->pjoin[k]) hipEventDestroy(s->pjoin[k]);
     }
+    if (s->pfork) hipEventDestroy(s->pfork);
     for (int k = 1; k < MCEIK_MAX_PIPES; k++) if (s->pws[k]) hipFree(s->pws[k]);
     for (void *p : s->allocs) hipFree(p);
     for (int i = 0; i < 2 * s->ev_made; i++) hipEventDestroy(s->ev[i]);
