@@ -248,7 +248,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     gather_check = None
-    if world > 1:
+    if world > 1 and comm is not None:
         # outside the timed region: the library gather == torch.distributed's gather
         tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=None if rehearse else dev)
         if rank == 0:
@@ -280,27 +280,35 @@ def main():
         alg_bytes = bricks * (n_nodes / nbricks) * bpn    # this rank's launches
         full_bytes = iters * 8.0 * n_nodes * bpn          # the same iterations without skipping
         avg_ms = fsm_ms / max(nlaunch, 1)
+        steps = max(args.steps, 1)
+        solves_per_step = per_gpu * p.nstat                 # this rank's (chain, station) solves
+        alg_step = alg_bytes / steps                        # algorithmic bytes of one step (all pipes)
         achieved = per_launch = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
-        pipes = round(nlaunch / max(args.steps, 1))       # 1 if the sampler fell back to one pipe
+        pipes = round(nlaunch / steps)                      # 1 if the sampler fell back to one pipe
         if pipes > 1:
             # two half launches per step, overlapped: a half's HIP-event span also
             # covers the time it waits for the other half's waves, so price one
             # step's algorithmic bytes on the step's wall time instead (includes
             # propose/accept and the gather: conservative)
             achieved = alg_bytes / elapsed / 1e9                  # this rank's bytes, the timed region
-        traffic = None
+        # the FSM time of one step: the single launch (HIP events) or, with pipes,
+        # the wall time per step (the overlapped half launches' union is shorter)
+        step_fsm_s = avg_ms * 1e-3 if pipes <= 1 else elapsed / steps
+        traffic = traffic_src = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
             if (tj.get("workload") == args.config and tj.get("chains_per_gpu") == per_gpu
                     and tj.get("kernel_rev") == KERNEL_REV and args.precision == 32):
-                traffic = tj.get("hbm_bytes_per_launch")
+                traffic = tj.get("hbm_bytes_per_launch")      # one single-pipe launch = one step
+                traffic_src = (f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of kernel_rev {KERNEL_REV} "
+                               f"({tj.get('source', 'profiles/traffic.json')}); not measured in this run")
         line = {
             "metric": METRIC,
             "value": round(total / elapsed, 3),
             "unit": "proposals/s",
-            "n_gpus": world,
+            "n_gpus": 1 if rehearse else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2),
@@ -321,22 +329,30 @@ def main():
                          "kernel_rev": KERNEL_REV,
                          "timing": (f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
                                     if pipes > 1 else "HIP events around each FSM launch"),
-                         "traffic_per": "step (= one single-pipe launch, profiles/traffic.json)",
-                         "alg_bytes_per_launch": alg_bytes / max(nlaunch, 1),
-                         "bytes_per_node_sweep": bpn, "avg_launch_ms": round(avg_ms, 3),
-                         "launches_per_step": round(nlaunch / max(args.steps, 1), 3),
+                         "per": "step: every per-unit field below is per step or per solve, whatever the pipes",
+                         "alg_bytes_per_step": alg_step,
+                         "traffic_per_step": traffic, "traffic_source": traffic_src,
+                         "traffic_over_alg": round(traffic / alg_step, 4) if traffic else None,
+                         "bytes_per_node_sweep": bpn,
+                         "fsm_s_per_step": round(step_fsm_s, 4),
+                         "launches_per_step": round(nlaunch / steps, 3), "avg_launch_ms": round(avg_ms, 3),
                          "frac_per_launch_events": round(per_launch / HBM_PEAK_GBS, 4),
-                         "iterations_per_solve": round(iters / max(nlaunch, 1) / (per_gpu * p.nstat), 3),
+                         "solves_per_step": solves_per_step,
+                         "iterations_per_solve": round(iters / steps / solves_per_step, 3),
                          "brick_visit_fraction": round(bricks / max(1.0, iters * 8.0 * nbricks), 4),
                          "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),
-                         "full_sweep_equiv_GBs": round(full_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9, 1)},
+                         "full_sweep_equiv_GBs": round(full_bytes / steps / step_fsm_s / 1e9, 1)},
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
         if rehearse:
+            line["ranks"] = world
             line["rehearsal"] = "one GPU shared by all ranks (MCEIK_BENCH_REHEARSAL=1): not a scaling measurement"
-        if gather_check is not None:
-            line["gather"] = {"path": gather_path, "equals_torch_gather": gather_check}
+        if world > 1:
+            line["gather"] = {"path": gather_path}
+            if gather_check is not None:
+                # the library's RCCL gather checked against torch.distributed's (outside the timed region)
+                line["gather"]["equals_torch_gather"] = gather_check
         if args.raw_stats:
             line["fsm_raw"] = {"bricks": bricks, "segs": segs, "segs_changed": segs_changed, "iters": iters,
                                "launches": nlaunch}

@@ -35,7 +35,27 @@ typedef struct mceik_mcmc_opts {
     int tt_interp;             /* event travel times: 0 = value at the event's nearest node (the
                                   reference's snapping, fsm3d.f90:697-711); 1 = trilinear
                                   interpolation in the event's grid cell (mceik_fsm_batch.ev_frac) */
+    int nphase;                /* velocity models per chain: 1 (or 0) = P only; 2 = joint P and S
+                                  (homog.c:208-258 makes both; the catalog's pickType selects the
+                                  model an observation is fit against, mceik_struct.h:4-8)   */
+    int vsmin, vsmax;          /* nphase 2: uniform prior on S cell velocity (m/s)          */
+    int mask_s;                /* nphase 1 and the catalog holds used S picks: 0 = init fails
+                                  (naming the count), 1 = fit the P picks and ignore the S picks */
 } mceik_mcmc_opts;
+
+/* What mceik_mcmc_init set up (diagnostic; mceik_mcmc_info). */
+typedef struct mceik_mcmc_info {
+    int npipe;                 /* chain groups on streams of their own (1 = one FSM launch per step) */
+    int nphase;                /* velocity models per chain (1 = P, 2 = P and S)              */
+    int step_z;                /* z nodes per macro step of the sampler's FSM kernel (16 or 8) */
+    int fixed_layout;          /* 1: the compile-time LDS layout instance                   */
+    int chains[4];             /* chains of pipe k (k < npipe)                               */
+    int waves[4];              /* resident FSM waves of pipe k's launch                     */
+    size_t workspace_bytes[4]; /* FSM scratch of pipe k                                     */
+    size_t lds_bytes;          /* LDS per FSM wave                                           */
+    int masked_s;              /* S observations ignored (nphase 1 with mask_s = 1)          */
+    char kernel[64];           /* the FSM kernel instance (rocprof name)                    */
+} mceik_mcmc_info;
 
 /* ---- run configuration (host only; csrc/parms.c) ----------------------
  * The reference's mains hard-code their parameters (homog.c:73-89,
@@ -57,8 +77,12 @@ int mceik_parms_args(int argc, char **argv, struct mceik_parms_struct *parms, mc
 /* Writes every key back in INI form (0 ok). */
 int mceik_parms_write(const char *path, const struct mceik_parms_struct *parms, const mceik_mcmc_opts *opts);
 
-/* v0: host [nchains][ncell] int m/s, ncell = ceil(nx/nrefx)*ceil(ny/nrefy)*
- * ceil(nz/nrefz), cell index x fastest.  Computes each chain's initial logL. */
+/* v0: host [nchains][nphase][ncell] int m/s (P model, then S model when
+ * nphase = 2), ncell = ceil(nx/nrefx)*ceil(ny/nrefy)*ceil(nz/nrefz), cell
+ * index x fastest.  Computes each chain's initial logL.  Returns 1 on invalid
+ * arguments (and on used S picks with nphase 1 unless mask_s), 2 when a
+ * station's solve fails (the reference's ierr), -1 on a device failure.
+ * Every array below sized [nchains][ncell] is [nchains][nphase][ncell]. */
 int mceik_mcmc_init(const struct mceik_parms_struct *parms,
                     const struct mceik_stations_struct *stations,
                     const struct mceik_catalog_struct *catalog,
@@ -78,9 +102,16 @@ int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long long *naccept
 int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_out, int max, int kind, int *nkept);
 /* Diagnostics of the last step: device pointers to the travel-time table
  * [nchains][nstat][nev] (fp32), per-solve iteration counts and reference ierr
- * [nchains][nstat] (int), and accept flags [nchains].  Any pointer may be NULL. */
+ * [nchains][nstat] (int), and accept flags [nchains].  With nphase 2 a step
+ * re-solves only the model its proposal changed: the tables are that phase's
+ * (mceik_mcmc_last_phase); after init they are [nchains][nphase][nstat][nev]
+ * and niter/ierr [nchains][nphase][nstat].  Any pointer may be NULL. */
 int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **niter, const unsigned char **accept,
                     const int **ierr);
+/* Device pointer to the last step's proposed phase per chain [nchains] (0 = P, 1 = S). */
+int mceik_mcmc_last_phase(mceik_mcmc *s, const int **phase);
+/* Fills *info (host). */
+int mceik_mcmc_get_info(mceik_mcmc *s, mceik_mcmc_info *info);
 /* Checkpoint / resume.  The proposal RNG is Philox keyed by (global chain,
  * step), so (v, logl, naccept, step, nkept) is the complete chain state:
  * restoring it into a sampler built with the same problem, seed and chain

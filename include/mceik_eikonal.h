@@ -103,7 +103,8 @@ typedef struct mceik_relocate_batch {
     int log_pdf;
     int nrows;                  /* rows of `tables` (> every obs_row) and nobs = ev_ptr[nev] on the
                                    host: single-pass kernel (each table value read once per launch,
-                                   LDS-staged); 0 = unknown, two passes per event from HBM */
+                                   LDS-staged; if ev_ptr[nev] != nobs or an obs_row >= nrows every
+                                   output is NaN); 0 = unknown, two passes per event from HBM */
     int nobs;
 } mceik_relocate_batch;
 int mceik_relocate(const mceik_relocate_batch *b, void *stream);
@@ -151,6 +152,10 @@ typedef struct mceik_fsm_batch {
                                    value at node ev_node (the reference's nearest-node snapping,
                                    fsm3d.f90:697-711).  Else trilinear interpolation in the cell whose
                                    lowest corner is ev_node (fp32, x then y then z, a + w*(b - a)) */
+    const int *model_phase;     /* slow_mode 1: device [nmodel] or NULL.  Non-NULL: model m solves the
+                                   slowness slow[(m*nphase + model_phase[m])*ncell ...] -- one of the
+                                   nphase models (P, S) a sampler chain holds; NULL: slow[m*ncell ...] */
+    int nphase;                 /* models per entry of `slow` when model_phase != NULL (1 or 2) */
 } mceik_fsm_batch;
 
 /* The batched extension of SURVEY s.8b with plain arguments: nmodels x

@@ -25,7 +25,7 @@ class FsmBatch(C.Structure):
                 ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
                 ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p),
                 ("max_waves", C.c_int), ("traffic", C.c_void_p), ("step_z", C.c_int),
-                ("ev_frac", C.c_void_p)]
+                ("ev_frac", C.c_void_p), ("model_phase", C.c_void_p), ("nphase", C.c_int)]
 
 
 class RelocateBatch(C.Structure):
@@ -74,7 +74,15 @@ class McmcOpts(C.Structure):
     _fields_ = [("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nchains", C.c_int),
                 ("chain_offset", C.c_int), ("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int),
                 ("seed", C.c_uint32), ("max_samples", C.c_int), ("device", C.c_int),
-                ("precision", C.c_int), ("max_waves", C.c_int), ("tt_interp", C.c_int)]
+                ("precision", C.c_int), ("max_waves", C.c_int), ("tt_interp", C.c_int),
+                ("nphase", C.c_int), ("vsmin", C.c_int), ("vsmax", C.c_int), ("mask_s", C.c_int)]
+
+
+class McmcInfo(C.Structure):
+    """mceik_mcmc_info (include/mceik.h)."""
+    _fields_ = [("npipe", C.c_int), ("nphase", C.c_int), ("step_z", C.c_int), ("fixed_layout", C.c_int),
+                ("chains", C.c_int * 4), ("waves", C.c_int * 4), ("workspace_bytes", C.c_size_t * 4),
+                ("lds_bytes", C.c_size_t), ("masked_s", C.c_int), ("kernel", C.c_char * 64)]
 
 
 # every extern "C" symbol include/*.h declares
@@ -86,7 +94,8 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_b
            "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
-           "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize",
+           "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize", "mceik_mcmc_last_phase",
+           "mceik_mcmc_get_info",
            "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write",
            "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather")
 
@@ -163,6 +172,10 @@ def lib():
     L.mceik_comm_finalize.argtypes = [C.POINTER(C.c_void_p)]
     L.mceik_mcmc_gather.restype = C.c_int
     L.mceik_mcmc_gather.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    L.mceik_mcmc_last_phase.restype = C.c_int
+    L.mceik_mcmc_last_phase.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    L.mceik_mcmc_get_info.restype = C.c_int
+    L.mceik_mcmc_get_info.argtypes = [C.c_void_p, C.POINTER(McmcInfo)]
     L.mceik_mcmc_finalize.restype = C.c_int
     L.mceik_mcmc_finalize.argtypes = [C.POINTER(C.c_void_p)]
     _lib = L

@@ -24,6 +24,7 @@ hipError_t fsm_zero_words(unsigned *p, int n, hipStream_t st);
 int fsm_occupancy(const FsmLaunch &L, int is_double);
 size_t fsm_launch_lds_bytes(const FsmLaunch &L, int is_double);
 int fsm_launch_kind(const FsmLaunch &L, int is_double);
+const char *fsm_launch_name(const FsmLaunch &L, int is_double);
 hipError_t fsm_to_brick_f64(const double *src, void *dst, int dst_double, const FsmLaunch &L, int nfield, hipStream_t st);
 hipError_t fsm_from_brick_f64(const void *src, int src_double, double *dst, const FsmLaunch &L, int nfield, hipStream_t st);
 hipError_t fsm_from_brick_f32(const float *src, float *dst, const FsmLaunch &L, int nfield, hipStream_t st);
@@ -93,6 +94,8 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.magic_ry = ((1u << 20) + L.nry - 1) / L.nry;
     L.magic_rz = ((1u << 20) + L.nrz - 1) / L.nrz;
     L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab; L.ev_frac = b->ev_frac;
+    L.model_phase = b->slow_mode == 1 ? b->model_phase : nullptr;
+    L.nphase = b->nphase > 0 ? b->nphase : 1;
     // LDS cell cache when every z-block's cells fit (2 x 2 x 8 at nref = 4, kb = 4)
     {
         auto span = [](int a, int e, int nr) { return e / nr - a / nr + 1; };
@@ -138,8 +141,10 @@ static int device_cus()
 }
 
 // Scratch budget for the per-wave u / u0 fields, fixed at the first call (so
-// workspace_bytes and batch_solve agree): MCEIK_FSM_WS_GB if set, else 80% of
-// the device's total memory (230 GB on a 288-GB MI355X).
+// workspace_bytes and batch_solve agree): MCEIK_FSM_WS_GB if set, else the
+// device memory free at that moment less an 8-GiB margin (the sampler's other
+// arrays, the caller's tensors), at most 80% of the total (230 GB on a 288-GB
+// MI355X).  A sampler with several pipes splits it between them (pipes_setup).
 static size_t ws_budget_bytes()
 {
     static size_t budget = 0;
@@ -150,8 +155,15 @@ static size_t ws_budget_bytes()
             budget = (size_t)(gb * 1073741824.0);
         } else {
             size_t fr = 0, tot = 0;
-            // at 256^3 (128 MiB of u + u0 per wave): 6.7 waves/CU (half: 4.2)
-            budget = hipMemGetInfo(&fr, &tot) == hipSuccess && tot ? tot / 5 * 4 : (size_t)96 << 30;
+            const size_t margin = (size_t)8 << 30;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot) {
+                // at 256^3 (128 MiB of u + u0 per wave): 6.7 waves/CU
+                budget = tot / 5 * 4;
+                const size_t avail = fr > 2 * margin ? fr - margin : fr / 2;
+                if (avail < budget) budget = avail;
+            } else {
+                budget = (size_t)96 << 30;
+            }
         }
     }
     return budget;
@@ -173,6 +185,14 @@ static int batch_waves(const FsmLaunch &L, int is_double)
         fprintf(stderr, "mceik fsm launch: %d-z steps, %d waves/CU (occupancy), %ld resident waves, %zu B LDS per wave\n",
                 fsm_launch_kind(L, is_double), per_cu, w, fsm_launch_lds_bytes(L, is_double));
     return (int)(w < 1 ? 1 : w);
+}
+
+// Waves of a batch before the scratch budget caps them.
+static int fsm_batch_waves_uncapped(const mceik_fsm_batch *b)
+{
+    FsmLaunch L;
+    fill_launch(L, b);
+    return batch_waves(L, b->precision == 64);
 }
 
 // Workspace: [8 queue heads, 1 KiB][slow brick copy (mode 0)][u scratch][u0 scratch]
@@ -988,9 +1008,13 @@ struct mceik_mcmc {
     hipEvent_t pfork, pjoin[MCEIK_MAX_PIPES];
     McmcDev pD[MCEIK_MAX_PIPES];
     mceik_fsm_batch pfb[MCEIK_MAX_PIPES];
-    void *pws[MCEIK_MAX_PIPES];        // pipe k's workspace (pipe 0 uses ws)
+    void *pws[MCEIK_MAX_PIPES];        // pipe k's workspace: a part of ws, ws itself, or its own
     size_t pws_bytes[MCEIK_MAX_PIPES];
-    mceik_fsm_batch fb;
+    bool pws_own[MCEIK_MAX_PIPES];     // pws[k] was allocated for the pipe
+    mceik_fsm_batch fb;                // a step's batch: every chain's proposed model x stations
+    mceik_fsm_batch fb_all;            // init / restore: every model of every chain (= fb with one model)
+    const float *last_ttab;            // tables of the last forward (mceik_mcmc_last)
+    int masked_s;                      // S picks ignored (nphase 1, mask_s)
     int device, max_samples, nburn, keepk, nkept, niter_total;
     int nkept_base;                    // nkept at the last restore: earlier states are not in the ring
     long long step;
@@ -1072,8 +1096,8 @@ static int fold_launch(mceik_mcmc *s, long long k)
 static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
 {
     mceik_fsm_batch &fb = pipe < 0 ? s->fb : s->pfb[pipe];
-    void *ws = pipe > 0 ? s->pws[pipe] : s->ws;
-    const size_t ws_bytes = pipe > 0 ? s->pws_bytes[pipe] : s->ws_bytes;
+    void *ws = pipe >= 0 ? s->pws[pipe] : s->ws;
+    const size_t ws_bytes = pipe >= 0 ? s->pws_bytes[pipe] : s->ws_bytes;
     const hipStream_t st = pipe < 0 ? s->stream : s->pst[pipe];
     int r = 0;
     if (timed) {
@@ -1091,6 +1115,7 @@ static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
         HIPCHK(hipEventRecord(s->ev[2 * r], st));
     }
     if (mceik_fsm_batch_solve(&fb, ws, ws_bytes, st)) return -1;
+    s->last_ttab = s->fb.ttab;
     if (timed) {
         HIPCHK(hipEventRecord(s->ev[2 * r + 1], st));
         s->nlaunch++;
@@ -1099,6 +1124,15 @@ static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
         HIPCHK(mcmc_lpt_order(s->d_clock, s->fb.nmodel * s->fb.nstat, s->d_order, s->stream));
         s->fb.solve_order = s->d_order;
     }
+    return 0;
+}
+
+// Untimed forward of every model of every chain (init, restore): tables into
+// ttab_cur (nphase 2) or the step tables (nphase 1).
+static int mcmc_forward_all(mceik_mcmc *s)
+{
+    if (mceik_fsm_batch_solve(&s->fb_all, s->ws, s->ws_bytes, s->stream)) return -1;
+    s->last_ttab = s->fb_all.ttab;
     return 0;
 }
 
@@ -1131,24 +1165,26 @@ static void clock_report(mceik_mcmc *s, const char *tag)
 static McmcDev dev_view(const McmcDev &D, int off, int n)
 {
     McmcDev V = D;
-    const size_t o = (size_t)off, oc = o * D.ncell;
+    const size_t o = (size_t)off, oc = o * D.ncm;
     V.nchains = n;
     V.chain_offset = D.chain_offset + off;
     V.v += oc; V.slow_cur += oc; V.slow_prop += oc;
     V.logl += o; V.naccept += o;
-    V.prop_cell += o; V.prop_v += o; V.prop_inprior += o; V.prop_logu += o; V.accept += o;
+    V.prop_cell += o; V.prop_phase += o; V.prop_v += o; V.prop_inprior += o; V.prop_logu += o; V.accept += o;
     V.ttab += o * D.nstat * D.nev;
+    if (V.ttab_cur) V.ttab_cur += o * D.nphase * D.nstat * D.nev;
     if (V.keep_v) V.keep_v += oc;
     if (V.keep_logl) V.keep_logl += o;
     return V;
 }
 
-static mceik_fsm_batch batch_view(const mceik_fsm_batch &b, int off, int n, size_t ncell)
+static mceik_fsm_batch batch_view(const mceik_fsm_batch &b, int off, int n, size_t ncm)
 {
     mceik_fsm_batch V = b;
     const size_t o = (size_t)off, os = o * b.nstat;
     V.nmodel = n;
-    V.slow = (const float *)b.slow + o * ncell;
+    V.slow = (const float *)b.slow + o * ncm;       // a chain's models are ncm = nphase * ncell floats
+    if (V.model_phase) V.model_phase = b.model_phase + o;
     V.ttab = b.ttab + os * b.nev;
     V.niter = b.niter + os;
     V.ierr = b.ierr + os;
@@ -1163,25 +1199,54 @@ static mceik_fsm_batch batch_view(const mceik_fsm_batch &b, int off, int n, size
 static int pipes_setup(mceik_mcmc *s, int np)
 {
     const int nch = s->D.nchains;
-    const size_t ncell = (size_t)s->D.ncell;
+    const size_t ncm = (size_t)s->D.ncm;
+    // the scratch budget binds (large grids): the pipes share the waves one
+    // pipe would keep, so every workspace together stays within the budget
+    const int w1 = ws_layout(&s->fb).nwaves;
+    const bool capped = w1 < (long long)fsm_batch_waves_uncapped(&s->fb);
     for (int k = 0; k < np; k++) {
         const int lo = (int)((long long)nch * k / np), hi = (int)((long long)nch * (k + 1) / np);
         s->pD[k] = dev_view(s->D, lo, hi - lo);
-        s->pfb[k] = batch_view(s->fb, lo, hi - lo, ncell);
+        s->pfb[k] = batch_view(s->fb, lo, hi - lo, ncm);
+        if (capped) {
+            const int share = w1 / np > 0 ? w1 / np : 1;
+            if (s->pfb[k].max_waves <= 0 || s->pfb[k].max_waves > share) s->pfb[k].max_waves = share;
+        }
     }
-    bool fit = mceik_fsm_workspace_bytes(&s->pfb[0]) <= s->ws_bytes;
+    // workspaces: carved out of the sampler's own when they fit in it together
+    // (budget-capped grids), else pipe 0 reuses it and the others get their own
+    size_t sum = 0;
+    for (int k = 0; k < np; k++) sum += (s->pws_bytes[k] = (mceik_fsm_workspace_bytes(&s->pfb[k]) + 255) & ~(size_t)255);
+    bool fit = true;
     size_t extra = 0;
-    for (int k = 1; k < np && fit; k++) {
-        s->pws_bytes[k] = mceik_fsm_workspace_bytes(&s->pfb[k]);
-        extra += s->pws_bytes[k];
-        if (hipMalloc(&s->pws[k], s->pws_bytes[k]) != hipSuccess) {
-            (void)hipGetLastError();
-            s->pws[k] = nullptr;
-            fit = false;
+    if (sum <= s->ws_bytes) {
+        size_t off = 0;
+        for (int k = 0; k < np; k++) {
+            s->pws[k] = (char *)s->ws + off;
+            s->pws_own[k] = false;
+            off += s->pws_bytes[k];
+        }
+    } else {
+        fit = s->pws_bytes[0] <= s->ws_bytes;
+        s->pws[0] = s->ws;
+        s->pws_bytes[0] = s->ws_bytes;
+        for (int k = 1; k < np && fit; k++) {
+            extra += s->pws_bytes[k];
+            if (hipMalloc(&s->pws[k], s->pws_bytes[k]) != hipSuccess) {
+                (void)hipGetLastError();
+                s->pws[k] = nullptr;
+                fit = false;
+            } else {
+                s->pws_own[k] = true;
+            }
         }
     }
     if (!fit) {
-        for (int k = 1; k < np; k++) if (s->pws[k]) { hipFree(s->pws[k]); s->pws[k] = nullptr; }
+        for (int k = 0; k < np; k++) {
+            if (s->pws_own[k] && s->pws[k]) hipFree(s->pws[k]);
+            s->pws[k] = nullptr;
+            s->pws_own[k] = false;
+        }
         fprintf(stderr, "mceik_mcmc_init: %d pipes need %zu B more FSM workspace; running one pipe\n", np, extra);
         return 0;
     }
@@ -1199,20 +1264,23 @@ static int pipes_setup(mceik_mcmc *s, int np)
 // would stay u_nan).  Synchronises; names the failing stations.
 static int check_forward_ierr(mceik_mcmc *s, const char *who)
 {
-    const size_t n = (size_t)s->D.nchains * s->D.nstat;
+    const int np = s->D.nphase, ns = s->D.nstat;
+    const size_t n = (size_t)s->D.nchains * np * ns;     // the full batch: [chain][phase][station]
     std::vector<int> ie(n);
     HIPCHK(hipStreamSynchronize(s->stream));
     HIPCHK(hipMemcpy(ie.data(), s->d_ierr, n * sizeof(int), hipMemcpyDeviceToHost));
     int bad = 0;
-    for (int st = 0; st < s->D.nstat; st++) {
-        int e = 0;
-        for (int c = 0; c < s->D.nchains && !e; c++) e = ie[(size_t)c * s->D.nstat + st];
-        if (e) {
-            fprintf(stderr, "%s: station %d (0-based): eikonal solve ierr = %d%s\n", who, st, e,
-                    e == 1 ? " (source on the grid's first node or outside it, fsm3d.f90:736-745)" : "");
-            bad = 1;
+    for (int ph = 0; ph < np; ph++)
+        for (int st = 0; st < ns; st++) {
+            int e = 0;
+            for (int c = 0; c < s->D.nchains && !e; c++) e = ie[((size_t)c * np + ph) * ns + st];
+            if (e) {
+                fprintf(stderr, "%s: station %d (0-based)%s: eikonal solve ierr = %d%s\n", who, st,
+                        np > 1 ? (ph ? ", S model" : ", P model") : "", e,
+                        e == 1 ? " (source on the grid's first node or outside it, fsm3d.f90:736-745)" : "");
+                bad = 1;
+            }
         }
-    }
     return bad;
 }
 
@@ -1226,9 +1294,11 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         fprintf(stderr, "mceik_mcmc_init: the eikonal solver needs dx = dy = dz\n");
         return 1;
     }
+    const int nphase = o->nphase <= 1 ? 1 : o->nphase;
     if (o->nx < 2 || o->ny < 2 || o->nz < 2 || o->nchains < 1 || st->nstat < 1 || cat->nevents < 1 ||
         o->vmin < 1 || o->vmax < o->vmin || o->dvmax < 1 || !(o->precision == 0 || o->precision == 32 ||
-                                                              o->precision == 64)) {
+                                                              o->precision == 64) ||
+        nphase > 2 || (nphase == 2 && (o->vsmin < 1 || o->vsmax < o->vsmin))) {
         fprintf(stderr, "mceik_mcmc_init: invalid options\n");
         return 1;
     }
@@ -1237,8 +1307,31 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
             fprintf(stderr, "mceik_mcmc_init: obsPtr must be non-decreasing\n");
             return 1;
         }
-    for (int j = 0; j < cat->obsPtr[cat->nevents]; j++)
-        if (cat->luseObs[j] != 0 && cat->pickType[j] == P_PRIMARY_PICK && !(cat->varObs[j] > 0.0)) {
+    const int nstat = st->nstat, nev = cat->nevents, nch = o->nchains;
+    const int nobs = cat->obsPtr[nev];
+    // observations fit: used P picks, and used S picks against the S model
+    // (nphase 2); a P-only sampler refuses a catalog with S picks unless told
+    // to ignore them (mask_s), so no observation disappears silently
+    int nsused = 0;
+    for (int j = 0; j < nobs; j++) {
+        const int k = cat->statPtr[j] - 1;
+        if (cat->luseObs[j] != 0 && cat->pickType[j] == S_PRIMARY_PICK && k >= 0 && k < nstat) nsused++;
+    }
+    if (nphase == 1 && nsused > 0) {
+        if (!o->mask_s) {
+            fprintf(stderr, "mceik_mcmc_init: the catalog holds %d used S picks; set nphase = 2 (joint P and S "
+                            "models) or mask_s = 1 (fit the P picks only)\n", nsused);
+            return 1;
+        }
+        fprintf(stderr, "mceik_mcmc_init: ignoring %d S picks (nphase 1, mask_s)\n", nsused);
+    }
+    auto fit_obs = [&](int j) {
+        const int k = cat->statPtr[j] - 1;
+        return cat->luseObs[j] != 0 && k >= 0 && k < nstat &&
+               (cat->pickType[j] == P_PRIMARY_PICK || (nphase == 2 && cat->pickType[j] == S_PRIMARY_PICK));
+    };
+    for (int j = 0; j < nobs; j++)
+        if (fit_obs(j) && !(cat->varObs[j] > 0.0)) {
             fprintf(stderr, "mceik_mcmc_init: observation %d has varObs <= 0\n", j);
             return 1;
         }
@@ -1249,6 +1342,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     s->stream = nullptr;
     s->step = 0;
     s->nkept = 0;
+    s->masked_s = nphase == 1 ? nsused : 0;
     s->nburn = parms->mcparms.nburnIn;
     s->keepk = parms->mcparms.keepK > 0 ? parms->mcparms.keepK : 1;
     s->niter_total = parms->mcparms.niter;
@@ -1257,12 +1351,14 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         nrz = parms->nrefz > 0 ? parms->nrefz : 1;
     int ncx = mceik_div_up(o->nx, nrx), ncy = mceik_div_up(o->ny, nry), ncz = mceik_div_up(o->nz, nrz);
     int ncell = ncx * ncy * ncz;
-    int nstat = st->nstat, nev = cat->nevents, nch = o->nchains;
+    const int ncm = ncell * nphase;
     McmcDev &D = s->D;
     memset(&D, 0, sizeof(D));
     D.nchains = nch; D.chain_offset = o->chain_offset; D.ncell = ncell; D.nstat = nstat; D.nev = nev;
+    D.nphase = nphase; D.ncm = ncm;
     D.keep_stride = nch;
     D.vmin = o->vmin; D.vmax = o->vmax; D.dvmax = o->dvmax; D.seed = o->seed;
+    D.vsmin = nphase == 2 ? o->vsmin : 0; D.vsmax = nphase == 2 ? o->vsmax : 0;
     // host-side problem tables
     std::vector<double> src((size_t)nstat * 4);
     for (int i = 0; i < nstat; i++) {
@@ -1283,17 +1379,19 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         }
         ev[e] = (iz * o->ny + iy) * o->nx + ix;
     }
-    int nobs = cat->obsPtr[nev];
-    std::vector<int> ostat(nobs > 0 ? nobs : 1), omask(nobs > 0 ? nobs : 1);
+    std::vector<int> ostat(nobs > 0 ? nobs : 1), omask(nobs > 0 ? nobs : 1), ophase(nobs > 0 ? nobs : 1);
     std::vector<double> tcorr(nobs > 0 ? nobs : 1);
     for (int j = 0; j < nobs; j++) {
         int k = cat->statPtr[j] - 1;
-        int use = cat->luseObs[j] != 0 && cat->pickType[j] == P_PRIMARY_PICK && k >= 0 && k < nstat;
+        int use = fit_obs(j);
+        int sph = use && cat->pickType[j] == S_PRIMARY_PICK;
         ostat[j] = use ? k : 0;
         omask[j] = !use;
-        tcorr[j] = (use && st->pcorr) ? st->pcorr[k] : 0.0;
+        ophase[j] = sph;
+        const double *corr = sph ? st->scorr : st->pcorr;       // static corrections (mceik_struct.h:42-44)
+        tcorr[j] = (use && corr) ? corr[k] : 0.0;
     }
-    std::vector<float> sl((size_t)nch * ncell);
+    std::vector<float> sl((size_t)nch * ncm);
     for (size_t i = 0; i < sl.size(); i++) sl[i] = 1.0f / (float)v0[i];
     int rc = 0;
     double *d_src = nullptr;
@@ -1305,34 +1403,40 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     float *d_evf = nullptr;
     if (o->tt_interp) rc |= dput(s, &d_evf, evf.data(), evf.size());
     rc |= dput(s, &d_optr, (const int *)cat->obsPtr, (size_t)nev + 1);
-    int *d_ostat = nullptr, *d_omask = nullptr;
+    int *d_ostat = nullptr, *d_omask = nullptr, *d_ophase = nullptr;
     double *d_tobs = nullptr, *d_tcorr = nullptr, *d_var = nullptr;
     rc |= dput(s, &d_ostat, ostat.data(), ostat.size());
     rc |= dput(s, &d_omask, omask.data(), omask.size());
+    rc |= dput(s, &d_ophase, ophase.data(), ophase.size());
     rc |= dput(s, &d_tobs, (const double *)cat->tobs, (size_t)(nobs > 0 ? nobs : 0));
     rc |= dput(s, &d_tcorr, tcorr.data(), tcorr.size());
     rc |= dput(s, &d_var, (const double *)cat->varObs, (size_t)(nobs > 0 ? nobs : 0));
-    rc |= dput(s, &D.v, v0, (size_t)nch * ncell);
+    rc |= dput(s, &D.v, v0, (size_t)nch * ncm);
     rc |= dput(s, &D.slow_cur, sl.data(), sl.size());
     rc |= dput(s, &D.slow_prop, sl.data(), sl.size());
     rc |= dalloc(s, &D.logl, nch);
     rc |= dalloc(s, &D.naccept, nch);
     rc |= dalloc(s, &D.prop_cell, nch);
+    rc |= dalloc(s, &D.prop_phase, nch);
     rc |= dalloc(s, &D.prop_v, nch);
     rc |= dalloc(s, &D.prop_inprior, nch);
     rc |= dalloc(s, &D.prop_logu, nch);
     rc |= dalloc(s, &D.accept, nch);
     rc |= dalloc(s, &d_tt, (size_t)nch * nstat * nev);
-    rc |= dalloc(s, &d_niter, (size_t)nch * nstat);
-    rc |= dalloc(s, &s->d_ierr, (size_t)nch * nstat);
+    if (nphase > 1) rc |= dalloc(s, &D.ttab_cur, (size_t)nch * nphase * nstat * nev);
+    rc |= dalloc(s, &d_niter, (size_t)nch * nphase * nstat);
+    rc |= dalloc(s, &s->d_ierr, (size_t)nch * nphase * nstat);
     rc |= dalloc(s, &s->d_iters, 4 + MCEIK_TRAFFIC_N);   // [0] iterations, [1..3] visit_stats, [4..] traffic
     if (s->max_samples) {
-        rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncell);
+        rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncm);
         rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
     }
     if (rc) { mceik_mcmc_finalize(&s); return -1; }
     D.ttab = d_tt; D.obs_ptr = d_optr; D.obs_stat = d_ostat; D.obs_mask = d_omask;
+    D.obs_phase = nphase > 1 ? d_ophase : nullptr;
     D.tobs = d_tobs; D.tcorr = d_tcorr; D.var = d_var;
+    // the step batch: one solve per (chain, station) of the model the proposal
+    // changed (model_phase = prop_phase: the other model's tables stay valid)
     mceik_fsm_batch &b = s->fb;
     memset(&b, 0, sizeof(b));
     b.nx = o->nx; b.ny = o->ny; b.nz = o->nz; b.h = parms->dx;
@@ -1341,6 +1445,8 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.precision = o->precision == 64 ? 64 : 32;
     b.nmodel = nch; b.nstat = nstat; b.nsrc = 1; b.src = d_src;
     b.slow_mode = 1; b.slow = D.slow_prop; b.nrx = nrx; b.nry = nry; b.nrz = nrz;
+    b.model_phase = nphase > 1 ? D.prop_phase : nullptr;
+    b.nphase = nphase;
     b.nev = nev; b.ev_node = d_ev; b.ev_frac = d_evf; b.ttab = d_tt; b.u_out = nullptr; b.niter = d_niter; b.ierr = s->d_ierr;
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
@@ -1348,10 +1454,21 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.traffic = s->d_iters + 4;
     b.max_waves = o->max_waves > 0 ? o->max_waves : 0;
     // f = h/v stays a normal float: the short correctly rounded sqrt (fp32 only)
-    b.fast_sqrt = b.precision == 32 && parms->dx / (double)o->vmax >= 1e-12 ? 1 : 0;
-    s->ws_bytes = mceik_fsm_workspace_bytes(&b);
+    const int vhi = nphase == 2 ? std::max(o->vmax, o->vsmax) : o->vmax;
+    b.fast_sqrt = b.precision == 32 && parms->dx / (double)vhi >= 1e-12 ? 1 : 0;
+    // the full batch (init, restore): every model of every chain, models
+    // [chain][phase] in place of model_phase, tables into ttab_cur
+    s->fb_all = b;
+    if (nphase > 1) {
+        s->fb_all.nmodel = nch * nphase;
+        s->fb_all.model_phase = nullptr;
+        s->fb_all.ttab = D.ttab_cur;
+    }
+    s->last_ttab = s->fb_all.ttab;
+    s->ws_bytes = std::max(mceik_fsm_workspace_bytes(&b), mceik_fsm_workspace_bytes(&s->fb_all));
     if (hipMalloc(&s->ws, s->ws_bytes) != hipSuccess) {
         fprintf(stderr, "mceik_mcmc_init: cannot allocate %zu B of FSM workspace\n", s->ws_bytes);
+        s->ws = nullptr;
         mceik_mcmc_finalize(&s);
         return -1;
     }
@@ -1366,7 +1483,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     const bool lpt = lpt_env && lpt_env[0] == '1';
     const char *rep_env = getenv("MCEIK_SOLVE_CLOCK_REPORT");
     const bool report = rep_env && rep_env[0] == '1';
-    if ((lpt || report) && dalloc(s, &s->d_clock, (size_t)nch * nstat * 2)) {
+    if ((lpt || report) && dalloc(s, &s->d_clock, (size_t)nch * nphase * nstat * 2)) {
         mceik_mcmc_finalize(&s);
         return -1;
     }
@@ -1374,10 +1491,12 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         mceik_mcmc_finalize(&s);
         return -1;
     }
-    unsigned long long *d_clock = s->d_clock;
-    b.solve_clock = d_clock;
+    b.solve_clock = s->d_clock;
     b.solve_order = nullptr;
-    if (mcmc_forward(s, false) || mcmc_init_loglik(D, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess) {
+    s->fb_all.solve_clock = s->d_clock;
+    s->fb_all.solve_order = nullptr;
+    if (mcmc_forward_all(s) || mcmc_init_loglik(D, s->stream) != hipSuccess ||
+        hipStreamSynchronize(s->stream) != hipSuccess) {
         mceik_mcmc_finalize(&s);
         return -1;
     }
@@ -1408,19 +1527,12 @@ extern "C" int mceik_mcmc_set_stream(mceik_mcmc *s, void *stream)
     return 0;
 }
 
-extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
+// Steps of one call.  Returns -1 on a HIP failure; the caller joins the pipes
+// whatever happened, so the caller's stream is always ordered after every
+// kernel this call queued on the internal streams.
+static int mcmc_steps(mceik_mcmc *s, int nsteps)
 {
-    if (!s) return 1;
-    if (nsteps < 0) {
-        const long long left = (long long)s->niter_total - s->step;
-        nsteps = left > 0 ? (int)left : 0;
-    }
-    DeviceScope dg(s->device);
     const int np = s->npipe;
-    if (np > 1) {                       // both pipes start after the caller's stream
-        HIPCHK(hipEventRecord(s->pfork, s->stream));
-        for (int k = 0; k < np; k++) HIPCHK(hipStreamWaitEvent(s->pst[k], s->pfork, 0));
-    }
     for (int i = 0; i < nsteps; i++) {
         uint64_t step = (uint64_t)s->step;
         int slot = -1;
@@ -1442,13 +1554,34 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
         if (s->report) clock_report(s, "step");
         s->step++;
     }
-    if (np > 1) {                       // the caller's stream continues after both
+    return 0;
+}
+
+extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
+{
+    if (!s) return 1;
+    if (nsteps < 0) {
+        const long long left = (long long)s->niter_total - s->step;
+        nsteps = left > 0 ? (int)left : 0;
+    }
+    DeviceScope dg(s->device);
+    const int np = s->npipe;
+    if (np > 1) {                       // both pipes start after the caller's stream
+        HIPCHK(hipEventRecord(s->pfork, s->stream));
+        for (int k = 0; k < np; k++) HIPCHK(hipStreamWaitEvent(s->pst[k], s->pfork, 0));
+    }
+    int rc = mcmc_steps(s, nsteps);
+    if (np > 1) {                       // the caller's stream continues after every pipe, also on failure
         for (int k = 0; k < np; k++) {
-            HIPCHK(hipEventRecord(s->pjoin[k], s->pst[k]));
-            HIPCHK(hipStreamWaitEvent(s->stream, s->pjoin[k], 0));
+            if (hipEventRecord(s->pjoin[k], s->pst[k]) != hipSuccess ||
+                hipStreamWaitEvent(s->stream, s->pjoin[k], 0) != hipSuccess) {
+                // cannot order the caller's stream after pipe k: wait for it here
+                if (hipStreamSynchronize(s->pst[k]) != hipSuccess) rc = -1;
+                rc = rc ? rc : -1;
+            }
         }
     }
-    return 0;
+    return rc;
 }
 
 extern "C" int mceik_mcmc_sync(mceik_mcmc *s)
@@ -1465,7 +1598,7 @@ extern "C" int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long lo
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
     const McmcDev &D = s->D;
-    if (v) HIPCHK(hipMemcpy(v, D.v, (size_t)D.nchains * D.ncell * 4, hipMemcpyDeviceToHost));
+    if (v) HIPCHK(hipMemcpy(v, D.v, (size_t)D.nchains * D.ncm * 4, hipMemcpyDeviceToHost));
     if (logl) HIPCHK(hipMemcpy(logl, D.logl, (size_t)D.nchains * 8, hipMemcpyDeviceToHost));
     if (naccept) HIPCHK(hipMemcpy(naccept, D.naccept, (size_t)D.nchains * 8, hipMemcpyDeviceToHost));
     if (step) *step = s->step;
@@ -1487,12 +1620,15 @@ extern "C" int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *log
     if (!s || !v || step < 0 || nkept < 0) return 1;
     DeviceScope dg(s->device);
     McmcDev &D = s->D;
-    const size_t n = (size_t)D.nchains * D.ncell;
-    for (size_t i = 0; i < n; i++)
-        if (v[i] < D.vmin || v[i] > D.vmax) {
-            fprintf(stderr, "mceik_mcmc_restore: v[%zu] = %d outside the prior [%d, %d]\n", i, v[i], D.vmin, D.vmax);
+    const size_t n = (size_t)D.nchains * D.ncm;
+    for (size_t i = 0; i < n; i++) {
+        const bool sph = (int)(i % (size_t)D.ncm) >= D.ncell;
+        const int lo = sph ? D.vsmin : D.vmin, hi = sph ? D.vsmax : D.vmax;
+        if (v[i] < lo || v[i] > hi) {
+            fprintf(stderr, "mceik_mcmc_restore: v[%zu] = %d outside the prior [%d, %d]\n", i, v[i], lo, hi);
             return 1;
         }
+    }
     std::vector<float> sl(n);
     for (size_t i = 0; i < n; i++) sl[i] = 1.0f / (float)v[i];
     HIPCHK(hipStreamSynchronize(s->stream));
@@ -1507,7 +1643,7 @@ extern "C" int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *log
         // one forward of the restored models (not timed, not counted in the FSM stats)
         unsigned long long keep[4 + MCEIK_TRAFFIC_N];
         HIPCHK(hipMemcpy(keep, s->d_iters, sizeof(keep), hipMemcpyDeviceToHost));
-        if (mcmc_forward(s, false)) return -1;
+        if (mcmc_forward_all(s)) return -1;
         HIPCHK(mcmc_init_loglik(D, s->stream));
         HIPCHK(hipStreamSynchronize(s->stream));
         HIPCHK(hipMemcpy(s->d_iters, keep, sizeof(keep), hipMemcpyHostToDevice));
@@ -1529,7 +1665,7 @@ extern "C" int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_o
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
     hipMemcpyKind k = kind ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    const size_t per = (size_t)s->D.nchains * s->D.ncell;
+    const size_t per = (size_t)s->D.nchains * s->D.ncm;
     // ring slot of the i-th of the n most recent states: (nkept - n + i) mod max_samples
     int i = 0;
     while (i < n) {
@@ -1553,14 +1689,14 @@ int mcmc_shard_view(mceik_mcmc *s, int which, McmcShard *out)
     if (!s || !out) return 1;
     const McmcDev &D = s->D;
     out->device = s->device; out->stream = s->stream;
-    out->nchains = D.nchains; out->chain_offset = D.chain_offset; out->ncell = D.ncell;
+    out->nchains = D.nchains; out->chain_offset = D.chain_offset; out->ncell = D.ncm;
     if (which == 0) {
         out->v = D.v; out->logl = D.logl;
         return 0;
     }
     if (s->max_samples <= 0 || s->nkept - s->nkept_base <= 0) return 1;
     const int slot = (int)(((long long)s->nkept - 1) % s->max_samples);
-    out->v = D.keep_v + (size_t)slot * D.nchains * D.ncell;
+    out->v = D.keep_v + (size_t)slot * D.nchains * D.ncm;
     out->logl = D.keep_logl + (size_t)slot * D.nchains;
     return 0;
 }
@@ -1569,10 +1705,41 @@ extern "C" int mceik_mcmc_last(mceik_mcmc *s, const float **ttab, const int **ni
                                const int **ierr)
 {
     if (!s) return 1;
-    if (ttab) *ttab = s->fb.ttab;
+    if (ttab) *ttab = s->last_ttab;
     if (niter) *niter = s->fb.niter;
     if (accept) *accept = s->D.accept;
     if (ierr) *ierr = s->d_ierr;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_last_phase(mceik_mcmc *s, const int **phase)
+{
+    if (!s || !phase) return 1;
+    *phase = s->D.prop_phase;
+    return 0;
+}
+
+extern "C" int mceik_mcmc_get_info(mceik_mcmc *s, mceik_mcmc_info *info)
+{
+    if (!s || !info) return 1;
+    DeviceScope dg(s->device);
+    memset(info, 0, sizeof(*info));
+    info->npipe = s->npipe;
+    info->nphase = s->D.nphase;
+    info->masked_s = s->masked_s;
+    FsmLaunch L;
+    fill_launch(L, &s->fb);
+    const int is_double = s->fb.precision == 64;
+    info->step_z = fsm_launch_kind(L, is_double);
+    info->fixed_layout = info->step_z == 16 && fsm16_fixed_layout(L) ? 1 : 0;
+    info->lds_bytes = fsm_launch_lds_bytes(L, is_double);
+    snprintf(info->kernel, sizeof(info->kernel), "%s", fsm_launch_name(L, is_double));
+    for (int k = 0; k < s->npipe && k < 4; k++) {
+        const mceik_fsm_batch &b = s->npipe > 1 ? s->pfb[k] : s->fb;
+        info->chains[k] = b.nmodel;
+        info->waves[k] = ws_layout(&b).nwaves;
+        info->workspace_bytes[k] = s->npipe > 1 ? s->pws_bytes[k] : s->ws_bytes;
+    }
     return 0;
 }
 
@@ -1626,7 +1793,7 @@ extern "C" int mceik_mcmc_finalize(mceik_mcmc **ps)
         if (s->pjoin[k]) hipEventDestroy(s->pjoin[k]);
     }
     if (s->pfork) hipEventDestroy(s->pfork);
-    for (int k = 1; k < MCEIK_MAX_PIPES; k++) if (s->pws[k]) hipFree(s->pws[k]);
+    for (int k = 0; k < MCEIK_MAX_PIPES; k++) if (s->pws_own[k] && s->pws[k]) hipFree(s->pws[k]);
     for (void *p : s->allocs) hipFree(p);
     for (int i = 0; i < 2 * s->ev_made; i++) hipEventDestroy(s->ev[i]);
     if (s->ws) hipFree(s->ws);

@@ -101,7 +101,7 @@ static bool on_device(const void *p, int dev)
 struct mceik_comm {
     ncclComm_t comm;
     int nranks, rank, device;
-    int *d_shard;          // [nranks][2] (chain_offset, nchains) exchange buffer
+    int *d_shard;          // [nranks][3] (chain_offset, nchains, local status) exchange buffer
     hipStream_t stream;    // the gather's own stream (non-blocking)
 };
 
@@ -143,7 +143,7 @@ extern "C" int mceik_comm_init(const unsigned char id[MCEIK_COMM_ID_BYTES], int 
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, u, rank);
-    hipError_t e = r == ncclSuccess ? hipMalloc(&c->d_shard, (size_t)nranks * 2 * sizeof(int)) : hipSuccess;
+    hipError_t e = r == ncclSuccess ? hipMalloc(&c->d_shard, (size_t)nranks * 3 * sizeof(int)) : hipSuccess;
     if (r == ncclSuccess && e == hipSuccess) {
         e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
         if (e != hipSuccess) hipFree(c->d_shard);
@@ -178,35 +178,75 @@ extern "C" int mceik_comm_finalize(mceik_comm **pc)
 // Collective.  Every rank's shard [chain_offset, chain_offset + nchains) is
 // sent to `root`, which receives it at its global position: point-to-point
 // send/recv in one RCCL group (shards may differ in size, no padding), the
-// root's own shard by a device copy.  The shards must tile [0, nchains_total)
-// (every rank checks the all-gathered (offset, count) table, so all return alike).
+// root's own shard by a device copy.  Every rank reaches the all-gather of the
+// (offset, count, local status) table whatever fails locally before it (device
+// mismatch, a failed sync, the root's staging allocation), and every rank
+// decides from the same table, so all return alike and none is left waiting
+// in a collective: the first nonzero local status in rank order, else 2 when
+// the shards do not tile [0, nchains_total), else the transfer's result.
 extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nchains_total, int root,
                                  int *v_out, double *logl_out)
 {
     if (!s || !c || root < 0 || root >= c->nranks || nchains_total < 1) return 1;
+    DevScope dg(c->device);
     McmcShard sh;
-    int have = mcmc_shard_view(s, which, &sh) == 0;
+    const int have = mcmc_shard_view(s, which, &sh) == 0;
+    int status = 0;
     if (sh.device != c->device) {
         fprintf(stderr, "mceik_mcmc_gather: sampler on device %d, communicator on %d\n", sh.device, c->device);
-        return 1;
+        status = 1;
     }
-    DevScope dg(c->device);
     // A checkpoint is synchronous: the sampler's queued steps finish first, then
     // the gather runs on the communicator's own stream with blocking host copies.
-    HIPCHK2(hipStreamSynchronize((hipStream_t)sh.stream));
+    if (!status && hipStreamSynchronize((hipStream_t)sh.stream) != hipSuccess) {
+        fprintf(stderr, "mceik_mcmc_gather: the sampler's stream failed\n");
+        status = -1;
+    }
+    const size_t ncell = (size_t)sh.ncell;
+    const size_t vbytes = (size_t)nchains_total * ncell * sizeof(int), lbytes = (size_t)nchains_total * sizeof(double);
+    // root: receive straight into caller device memory on this GPU, else into a
+    // staging buffer allocated before the collective starts
+    int *d_v = nullptr;
+    double *d_l = nullptr;
+    bool stage_v = false, stage_l = false;
+    if (!status && c->rank == root) {
+        stage_v = !on_device(v_out, c->device);
+        stage_l = !on_device(logl_out, c->device);
+        if (stage_v && hipMalloc((void **)&d_v, vbytes) != hipSuccess) { d_v = nullptr; status = -1; }
+        if (!stage_v) d_v = v_out;
+        if (!status && stage_l && hipMalloc((void **)&d_l, lbytes) != hipSuccess) { d_l = nullptr; status = -1; }
+        if (!stage_l) d_l = logl_out;
+        if (status) fprintf(stderr, "mceik_mcmc_gather: cannot allocate the root's staging buffers\n");
+    }
+    auto release = [&]() {
+        if (stage_v && d_v) hipFree(d_v);
+        if (stage_l && d_l) hipFree(d_l);
+    };
     hipStream_t st = c->stream;
-    // 1. every rank learns every shard (a rank without a kept state sends count -1)
-    const int mine[2] = {sh.chain_offset, have ? sh.nchains : -1};
-    std::vector<int> all((size_t)c->nranks * 2);
-    int rc = 0;
-    HIPCHK2(hipMemcpy(c->d_shard + 2 * c->rank, mine, sizeof(mine), hipMemcpyHostToDevice));
-    RCCLCHK(rccl().AllGather(c->d_shard + 2 * c->rank, c->d_shard, 2, ncclInt32, c->comm, st));
-    HIPCHK2(hipStreamSynchronize(st));
-    HIPCHK2(hipMemcpy(all.data(), c->d_shard, all.size() * sizeof(int), hipMemcpyDeviceToHost));
+    // 1. every rank learns every shard and status (a rank without a kept state
+    // sends count -1)
+    const int mine[3] = {sh.chain_offset, have ? sh.nchains : -1, status};
+    std::vector<int> all((size_t)c->nranks * 3);
+    if (hipMemcpy(c->d_shard + 3 * c->rank, mine, sizeof(mine), hipMemcpyHostToDevice) != hipSuccess ||
+        rccl().AllGather(c->d_shard + 3 * c->rank, c->d_shard, 3, ncclInt32, c->comm, st) != ncclSuccess ||
+        hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(all.data(), c->d_shard, all.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+        fprintf(stderr, "mceik_mcmc_gather: the shard-table all-gather failed\n");
+        release();
+        return -1;
+    }
+    for (int r = 0; r < c->nranks; r++)
+        if (all[3 * r + 2]) {
+            if (c->rank == root && r != c->rank)
+                fprintf(stderr, "mceik_mcmc_gather: rank %d failed locally (%d)\n", r, all[3 * r + 2]);
+            release();
+            return all[3 * r + 2];
+        }
     {   // the shards must tile [0, nchains_total): every rank checks the same table
+        int rc = 0;
         std::vector<int> cover((size_t)nchains_total, 0);
         for (int r = 0; r < c->nranks && !rc; r++) {
-            const int off = all[2 * r], n = all[2 * r + 1];
+            const int off = all[3 * r], n = all[3 * r + 1];
             if (n < 0 || off < 0 || (long long)off + n > nchains_total) { rc = 2; break; }
             for (int k = off; k < off + n; k++) cover[k]++;
         }
@@ -215,32 +255,16 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
             if (c->rank == root)
                 fprintf(stderr, "mceik_mcmc_gather: the ranks' shards (or kept states) do not tile [0, %d)\n",
                         nchains_total);
+            release();
             return rc;
         }
-    }
-    const size_t ncell = (size_t)sh.ncell;
-    const size_t vbytes = (size_t)nchains_total * ncell * sizeof(int), lbytes = (size_t)nchains_total * sizeof(double);
-    // root: receive straight into caller device memory on this GPU, else into a staging buffer
-    int *d_v = nullptr;
-    double *d_l = nullptr;
-    bool stage_v = false, stage_l = false;
-    if (c->rank == root) {
-        stage_v = !on_device(v_out, c->device);
-        stage_l = !on_device(logl_out, c->device);
-        if (stage_v) HIPCHK2(hipMalloc((void **)&d_v, vbytes));
-        else d_v = v_out;
-        if (stage_l && hipMalloc((void **)&d_l, lbytes) != hipSuccess) {
-            if (stage_v) hipFree(d_v);
-            return -1;
-        }
-        if (!stage_l) d_l = logl_out;
     }
     // 2. shards to the root (one RCCL group), the root's own by a device copy
     bool ok = rccl().GroupStart() == ncclSuccess;
     if (c->rank == root) {
         for (int r = 0; r < c->nranks && ok; r++) {
             if (r == root) continue;
-            const size_t off = (size_t)all[2 * r], n = (size_t)all[2 * r + 1];
+            const size_t off = (size_t)all[3 * r], n = (size_t)all[3 * r + 1];
             ok = rccl().Recv(d_v + off * ncell, n * ncell, ncclInt32, r, c->comm, st) == ncclSuccess &&
                  rccl().Recv(d_l + off, n, ncclFloat64, r, c->comm, st) == ncclSuccess;
         }
@@ -261,8 +285,7 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
         if (stage_v && v_out) ok = hipMemcpy(v_out, d_v, vbytes, hipMemcpyDeviceToHost) == hipSuccess;
         if (ok && stage_l && logl_out) ok = hipMemcpy(logl_out, d_l, lbytes, hipMemcpyDeviceToHost) == hipSuccess;
     }
-    if (stage_v) hipFree(d_v);
-    if (stage_l) hipFree(d_l);
+    release();
     if (!ok) {
         fprintf(stderr, "mceik_mcmc_gather: RCCL or copy failure\n");
         return -1;

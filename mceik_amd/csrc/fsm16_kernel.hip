@@ -868,7 +868,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         float *u = reinterpret_cast<float *>(L.u) + slot * L.field_elems;
         float *u0 = reinterpret_cast<float *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
         const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
-        const void *slow_model = reinterpret_cast<const float *>(L.slow) + (size_t)model * ncell;
+        const void *slow_model = reinterpret_cast<const float *>(L.slow) + fsm_slow_entry(L, model) * ncell;
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
                    sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
         // Before the first sweep every block counts as visited and unchanged

@@ -55,7 +55,15 @@ struct FsmLaunch {
     unsigned long long *traffic; // [MCEIK_TRAFFIC_N] requested bytes by category (MCEIK_TRAFFIC builds), or null
     int step_z;                  // host only: 8 forces the 8-z kernel, 0 = the launch's choice
     const float *ev_frac;        // [nev][3] trilinear fractions (ev_node = lowest corner), or null = node value
+    const int *model_phase;      // slow_mode 1: model m uses slow entry m * nphase + model_phase[m], or null
+    int nphase;
 };
+
+// Inversion-grid slowness entry of model m (slow_mode 1).
+static inline __host__ __device__ size_t fsm_slow_entry(const FsmLaunch &L, int m)
+{
+    return L.model_phase ? (size_t)m * L.nphase + L.model_phase[m] : (size_t)m;
+}
 
 static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
 

@@ -918,7 +918,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             slow_bytes = fbytes;
         } else {
             const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
-            slow_model = reinterpret_cast<const float *>(L.slow) + (size_t)model * ncell;
+            slow_model = reinterpret_cast<const float *>(L.slow) + fsm_slow_entry(L, model) * ncell;
             slow_bytes = (uint32_t)(ncell * 4);
         }
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
@@ -1123,6 +1123,25 @@ size_t fsm_launch_lds_bytes(const FsmLaunch &L, int is_double)
     return use_fsm16(L, is_double) ? fsm16_lds_bytes(L) : fsm_lds_bytes(L, is_double ? 8 : 4);
 }
 int fsm_launch_kind(const FsmLaunch &L, int is_double) { return use_fsm16(L, is_double) ? 16 : 8; }
+// The kernel instance a launch runs (names as in the rocprof traces).
+const char *fsm_launch_name(const FsmLaunch &L, int is_double)
+{
+    if (use_fsm16(L, is_double))
+        return fsm16_fixed_layout(L) ? "fsm16_solve_kernel<2, 1>" : L.ccb <= 64 ? "fsm16_solve_kernel<0, 1>"
+                                                                                 : "fsm16_solve_kernel<0, 4>";
+    switch (variant(L, is_double)) {
+    case 0: return "fsm_solve_kernel<float, 0, false, -1, 1, 0>";
+    case 2: return "fsm_solve_kernel<float, 1, false, -1, 1, 0>";
+    case 4: return "fsm_solve_kernel<float, 2, false, -1, 4, 0>";
+    case 5: return "fsm_solve_kernel<float, 2, true, -1, 4, 0>";
+    case 7: return "fsm_solve_kernel<float, 2, true, 2, 1, 0>";
+    case 8: return "fsm_solve_kernel<float, 2, true, 2, 1, 4>";
+    case 9: return "fsm_solve_kernel<double, 0, false, -1, 1, 0>";
+    case 11: return "fsm_solve_kernel<double, 1, false, -1, 1, 0>";
+    case 13: return "fsm_solve_kernel<double, 2, false, -1, 4, 0>";
+    }
+    return "?";
+}
 
 // Zeroes the launch's work-queue heads with a kernel rather than
 // hipMemsetAsync: inside a captured HIP graph the memset node was not replayed

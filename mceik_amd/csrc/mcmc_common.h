@@ -5,19 +5,25 @@
 
 struct McmcDev {
     int nchains, chain_offset, ncell, nstat, nev;
-    int vmin, vmax, dvmax;
+    int nphase;                    // velocity models per chain: 1 (P) or 2 (P, S)
+    int ncm;                       // ncell * nphase: one chain's model entries
+    int vmin, vmax, dvmax;         // P prior, proposal step
+    int vsmin, vsmax;              // S prior (nphase 2)
     uint32_t seed;
-    int *v;                        // [nchains][ncell] current model (m/s)
-    float *slow_cur, *slow_prop;   // [nchains][ncell] 1/v of current / proposed
+    int *v;                        // [nchains][nphase][ncell] current models (m/s)
+    float *slow_cur, *slow_prop;   // [nchains][nphase][ncell] 1/v of current / proposed
     double *logl;                  // [nchains]
     long long *naccept;            // [nchains]
-    int *prop_cell, *prop_v, *prop_inprior;
+    int *prop_cell, *prop_v, *prop_inprior;   // prop_cell indexes the chain's [nphase][ncell] entries
+    int *prop_phase;               // [nchains] the model the proposal changes (cell / ncell)
     double *prop_logu;
     unsigned char *accept;         // [nchains] last step
-    const float *ttab;             // [nchains][nstat][nev]
+    const float *ttab;             // [nchains][nstat][nev]: the proposed model's tables (its phase)
+    float *ttab_cur;               // nphase 2: [nchains][nphase][nstat][nev] tables of the current models
     const int *obs_ptr, *obs_stat, *obs_mask;
+    const int *obs_phase;          // [nobs] 0 = P, 1 = S (null: all P)
     const double *tobs, *tcorr, *var;
-    int *keep_v;                   // [max_samples][keep_stride][ncell]
+    int *keep_v;                   // [max_samples][keep_stride][nphase][ncell]
     double *keep_logl;             // [max_samples][keep_stride]
     int keep_stride;               // chains per kept slot: the sampler's nchains (a pipe's view covers a part)
 };
@@ -28,7 +34,7 @@ struct mceik_mcmc;
 struct McmcShard {
     int device, nchains, chain_offset, ncell;
     void *stream;
-    const int *v;                  // device [nchains][ncell]
+    const int *v;                  // device [nchains][ncell] (ncell = the chain's model entries)
     const double *logl;            // device [nchains]
 };
 int mcmc_shard_view(mceik_mcmc *s, int which, McmcShard *out);

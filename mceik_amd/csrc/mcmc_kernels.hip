@@ -41,46 +41,60 @@ __device__ __forceinline__ double det_log(double x)
     return de * 6.93147180369123816490e-01 + (2.0 * s * p + de * 1.90821492927058770002e-10);
 }
 
-// One proposal per chain: a single inversion cell moves by +-[1, dvmax] m/s.
-// slow_prop (== slow_cur everywhere but the proposed cell) gets the new cell.
+// One proposal per chain: a single inversion cell of one of the chain's
+// nphase models moves by +-[1, dvmax] m/s (cell drawn over [0, nphase*ncell):
+// with one model exactly the P-only draw).  slow_prop (== slow_cur everywhere
+// but the proposed cell) gets the new cell.
 __global__ void propose_kernel(McmcDev D, uint64_t step)
 {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= D.nchains) return;
     uint32_t ctr[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0u, 0u};
     philox4x32_10(ctr, (uint32_t)(D.chain_offset + c), D.seed);
-    int cell = (int)(((uint64_t)ctr[0] * (uint32_t)D.ncell) >> 32);
+    int cell = (int)(((uint64_t)ctr[0] * (uint32_t)D.ncm) >> 32);
     int mag = 1 + (int)(((uint64_t)ctr[1] * (uint32_t)D.dvmax) >> 32);
-    int vold = D.v[(size_t)c * D.ncell + cell];
+    const int ph = cell >= D.ncell ? 1 : 0;
+    int vold = D.v[(size_t)c * D.ncm + cell];
     int vn = vold + ((ctr[2] & 1u) ? -mag : mag);
-    int inp = vn >= D.vmin && vn <= D.vmax;
+    int inp = ph ? (vn >= D.vsmin && vn <= D.vsmax) : (vn >= D.vmin && vn <= D.vmax);
     D.prop_cell[c] = cell;
+    D.prop_phase[c] = ph;
     D.prop_v[c] = vn;
     D.prop_inprior[c] = inp;
     D.prop_logu[c] = det_log(((double)ctr[3] + 0.5) * (1.0 / 4294967296.0));
-    if (inp) D.slow_prop[(size_t)c * D.ncell + cell] = 1.0f / (float)vn;
+    if (inp) D.slow_prop[(size_t)c * D.ncm + cell] = 1.0f / (float)vn;
 }
 
 // logL = -sum_e objfn_e, objfn_e the L2 misfit with analytic origin time
-// (locate.c:923-1047 at one grid point, iwantOT = 1), observations in CSR order.
-__device__ double chain_loglik(const McmcDev &D, int c)
+// (locate.c:923-1047 at one grid point, iwantOT = 1), observations in CSR
+// order; an S observation is fit against the S model's table of its station
+// (the locator stacks both phases, locate.f90:399,442).  Tables of phase pph
+// come from the proposal's tables, the others from the current ones (pph < 0:
+// every phase from ttab_cur; nphase 1 uses pph = 0).
+__device__ double chain_loglik(const McmcDev &D, int c, int pph)
 {
-    const float *tt = D.ttab + (size_t)c * D.nstat * D.nev;
+    const float *tp = D.ttab + (size_t)c * D.nstat * D.nev;
+    const float *tcur = D.ttab_cur ? D.ttab_cur + (size_t)c * D.nphase * D.nstat * D.nev : nullptr;
     const double sqrt2i = 0.7071067811865475;
     double logl = 0.0;
+    auto te_of = [&](int j, int e) -> double {
+        const int ph = D.obs_phase ? D.obs_phase[j] : 0;
+        const size_t k = (size_t)D.obs_stat[j] * D.nev + e;
+        return (double)(ph == pph ? tp[k] : tcur[(size_t)ph * D.nstat * D.nev + k]);
+    };
     for (int e = 0; e < D.nev; e++) {
         int j0 = D.obs_ptr[e], j1 = D.obs_ptr[e + 1];
         double xnorm = 0.0, t0 = 0.0, obj = 0.0;
         for (int j = j0; j < j1; j++) if (!D.obs_mask[j]) xnorm = xnorm + 1.0 / D.var[j];
         for (int j = j0; j < j1; j++) {
             if (D.obs_mask[j]) continue;
-            double te = (double)tt[(size_t)D.obs_stat[j] * D.nev + e];
+            double te = te_of(j, e);
             double tc = D.tobs[j] - D.tcorr[j];
             t0 = t0 + ((1.0 / D.var[j]) / xnorm) * (tc - te);
         }
         for (int j = j0; j < j1; j++) {
             if (D.obs_mask[j]) continue;
-            double te = (double)tt[(size_t)D.obs_stat[j] * D.nev + e];
+            double te = te_of(j, e);
             double tc = D.tobs[j] - D.tcorr[j];
             double res = ((1.0 / D.var[j]) * sqrt2i) * (tc - (te + t0));
             obj = obj + res * res;
@@ -94,26 +108,34 @@ __global__ void init_loglik_kernel(McmcDev D)
 {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= D.nchains) return;
-    D.logl[c] = chain_loglik(D, c);
+    D.logl[c] = chain_loglik(D, c, D.nphase > 1 ? -1 : 0);
 }
 
 // Metropolis accept/reject; keeps slow_cur/slow_prop identical except while a
-// proposal is pending, so each step touches one cell per chain.
+// proposal is pending, so each step touches one cell per chain.  With two
+// models an accepted proposal's tables become its phase's current tables.
 __global__ void accept_kernel(McmcDev D, int keep_slot)
 {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= D.nchains) return;
     int cell = D.prop_cell[c];
-    size_t ci = (size_t)c * D.ncell + cell;
+    size_t ci = (size_t)c * D.ncm + cell;
     int acc = 0;
     if (D.prop_inprior[c]) {
-        double ln = chain_loglik(D, c);
+        const int ph = D.prop_phase[c];
+        double ln = chain_loglik(D, c, ph);
         acc = D.prop_logu[c] < ln - D.logl[c];
         if (acc) {
             D.logl[c] = ln;
             D.v[ci] = D.prop_v[c];
             D.slow_cur[ci] = D.slow_prop[ci];
             D.naccept[c] += 1;
+            if (D.nphase > 1) {
+                const size_t n = (size_t)D.nstat * D.nev;
+                const float *src = D.ttab + (size_t)c * n;
+                float *dst = D.ttab_cur + ((size_t)c * D.nphase + ph) * n;
+                for (size_t k = 0; k < n; k++) dst[k] = src[k];
+            }
         } else {
             D.slow_prop[ci] = D.slow_cur[ci];
         }
@@ -122,11 +144,11 @@ __global__ void accept_kernel(McmcDev D, int keep_slot)
     if (keep_slot >= 0) D.keep_logl[(size_t)keep_slot * D.keep_stride + c] = D.logl[c];
 }
 
-// Kept state copy: [slot][chain][cell] int (after accept_kernel).
+// Kept state copy: [slot][chain][nphase][ncell] int (after accept_kernel).
 __global__ void keep_kernel(McmcDev D, int keep_slot)
 {
-    size_t n = (size_t)D.nchains * D.ncell;
-    int *dst = D.keep_v + (size_t)keep_slot * D.keep_stride * D.ncell;
+    size_t n = (size_t)D.nchains * D.ncm;
+    int *dst = D.keep_v + (size_t)keep_slot * D.keep_stride * D.ncm;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = D.v[i];
 }
@@ -220,27 +242,47 @@ __global__ __launch_bounds__(TG) void relocate_lds_kernel(int ldgrd, int ngrd, i
     int *srow = (int *)(sw1 + cap), *soff = srow + cap;    // soff [nev + 1]
     const float sqrt2i = 0.7071067811865475f;
     const int tid = threadIdx.x;
+    __shared__ int bad;                                 // the caller's nobs / nrows do not hold
     if (tid == 0) {
-        int o = 0;
-        for (int e = 0; e < nev; e++) {
+        int o = 0, b = ev_ptr[0] != 0 || ev_ptr[nev] != nobs;
+        for (int e = 0; e < nev && !b; e++) {
+            b = ev_ptr[e + 1] < ev_ptr[e];
             soff[e] = o;
             o += (ev_ptr[e + 1] - ev_ptr[e] + 3) & ~3;
         }
         soff[nev] = o;
+        bad = b;
     }
     __syncthreads();
-    for (int e = 0; e < nev; e++) {
-        const float xn = xnorm[e];
-        const int j0 = ev_ptr[e], base = soff[e] - j0;
-        for (int j = j0 + tid; j < ev_ptr[e + 1]; j += TG) {
-            stc[base + j] = tc[j];
-            sw0[base + j] = wt[j] / xn;
-            sw1[base + j] = wt[j] * sqrt2i;
-            srow[base + j] = obs_row[j] * TG;
+    if (!bad) {
+        int b = 0;
+        for (int e = 0; e < nev; e++) {
+            const float xn = xnorm[e];
+            const int j0 = ev_ptr[e], base = soff[e] - j0;
+            for (int j = j0 + tid; j < ev_ptr[e + 1]; j += TG) {
+                const int r = obs_row[j];
+                b |= r < 0 || r >= nrows;
+                stc[base + j] = tc[j];
+                sw0[base + j] = wt[j] / xn;
+                sw1[base + j] = wt[j] * sqrt2i;
+                srow[base + j] = (b ? 0 : r) * TG;
+            }
         }
+        if (b) bad = 1;
     }
     const int g = blockIdx.x * TG + tid;
     const bool in = g < ngrd;
+    __syncthreads();
+    if (bad) {
+        // contract violated: every output of the block is NaN (no LDS access
+        // out of bounds, and no plausible-looking misfits)
+        if (in)
+            for (int e = 0; e < nev; e++) {
+                if (t0) t0[(size_t)e * ldgrd + g] = __builtin_nanf("");
+                objfn[(size_t)e * ldgrd + g] = __builtin_nanf("");
+            }
+        return;
+    }
     for (int r = 0; r < nrows; r++) tile[r * TG + tid] = in ? test[(size_t)ldgrd * r + g] : 0.0f;
     __syncthreads();
     if (!in) return;

@@ -167,16 +167,19 @@ def init_locations(dirnm, projnm, nx, ny, nz, nmodels, nevents, x0, y0, z0, dx, 
 
 
 def write_posterior(p, models, dirnm, projnm, device=0, relocate_events=True):
-    """Write kept velocity models (int32 [k, ncell] inversion-cell velocities,
-    e.g. the gathered Sampler.samples()) as the reference's HDF5 posterior:
-    the P travel-time table of every model x station (fp32 GPU forward, the
-    sampler's arithmetic; S tables stay empty: the sampler inverts one P
-    model) and, if `relocate_events`, every event's log joint PDF on the
-    grid for every model (GPU relocation over the event's observations in
-    catalog order, masked picks excluded).  Returns the two file names."""
+    """Write kept velocity models (int32 [k, ncell] inversion-cell P velocities,
+    or [k, 2, ncell] P and S models of a joint sampler, e.g. the gathered
+    Sampler.samples()) as the reference's HDF5 posterior: the P travel-time
+    table (and, with S models, the S table: PTravelTimes / STravelTimes,
+    h5io.c:662-697) of every model x station (fp32 GPU forward, the sampler's
+    arithmetic) and, if `relocate_events`, every event's log joint PDF on the
+    grid for every model (GPU relocation over the event's fitted observations
+    in catalog order -- an S pick against its station's S table -- masked
+    picks excluded).  Returns the two file names."""
     import torch
     from . import eikonal
-    models = np.asarray(models, dtype=np.int32).reshape(-1, p.ncell)
+    nph = int(getattr(p, "nphase", 1))
+    models = np.asarray(models, dtype=np.int32).reshape(-1, nph, p.ncell)
     nm = models.shape[0]
     dev = torch.device("cuda", device)
     nxyz = p.nx * p.ny * p.nz
@@ -184,20 +187,22 @@ def write_posterior(p, models, dirnm, projnm, device=0, relocate_events=True):
     bs = eikonal.BatchSolver(p.nx, p.ny, p.nz, p.h, p.x0, p.y0, p.z0, p.maxit, p.tol, 32, nref=p.nref)
     events = []
     mask_all, tcorr_all = p.obs_mask, p.tcorr
+    row_all = p.obs_stat + p.nstat * (p.obs_phase if nph > 1 else 0)   # table row: phase-major
     for e in range(p.nevents):
         k = np.arange(p.obs_ptr[e], p.obs_ptr[e + 1])
-        events.append(dict(rows=p.obs_stat[k], tobs=np.float32(p.tobs[k]), varobs=np.float32(p.var[k]),
+        events.append(dict(rows=row_all[k], tobs=np.float32(p.tobs[k]), varobs=np.float32(p.var[k]),
                            tcorr=np.float32(tcorr_all[k]), mask=np.int32(mask_all[k])))
     ttf = init_ttables(dirnm, projnm, p.nx, p.ny, p.nz, nm, p.nstat, p.x0, p.y0, p.z0, p.h, p.h, p.h)
     locf = init_locations(dirnm, projnm, p.nx, p.ny, p.nz, nm, p.nevents, p.x0, p.y0, p.z0, p.h, p.h, p.h) \
         if relocate_events else None
     try:
         for m in range(nm):
-            slow = torch.tensor((1.0 / models[m].astype(np.float32)).astype(np.float32).reshape(1, -1), device=dev)
-            u = bs.solve(src, slow, want_fields=True)["u"].reshape(p.nstat, nxyz)
+            slow = torch.tensor((1.0 / models[m].astype(np.float32)).astype(np.float32).reshape(nph, -1), device=dev)
+            u = bs.solve(src, slow, want_fields=True)["u"].reshape(nph * p.nstat, nxyz)
             host = u.cpu().numpy()
-            for s in range(p.nstat):
-                ttf.write_ttimes(s + 1, m + 1, host[s])
+            for ph in range(nph):
+                for s in range(p.nstat):
+                    ttf.write_ttimes(s + 1, m + 1, host[ph * p.nstat + s], iphase=ph + 1)
             if locf is not None:
                 logp, _ = eikonal.relocate(u.contiguous(), events, log_pdf=True)
                 logp = logp[:, :nxyz].cpu().numpy()

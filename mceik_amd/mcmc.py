@@ -54,12 +54,18 @@ class Problem:
     vmin: int = 1500
     vmax: int = 9000
     dvmax: int = 50
+    nphase: int = 1                 # velocity models per chain: 1 = P, 2 = P and S (homog.c:208-258)
+    vsmin: int = 800                # S prior (nphase 2)
+    vsmax: int = 5500
+    mask_s: int = 0                 # nphase 1: ignore used S picks instead of refusing the catalog
+    scorr: np.ndarray = None        # S static corrections (mceik_stations_struct.scorr)
     seed: int = 2016
     nburn: int = 0
     keepk: int = 1
     niter: int = 0                  # mcparms.niter: total proposals (Sampler.run(-1) runs the rest)
     tt_interp: int = 0              # 0: event times at the nearest node (reference); 1: trilinear in the cell
     v_true: np.ndarray = None       # [ncell] int, model used to make the picks
+    vs_true: np.ndarray = None      # [ncell] int, S model of the picks (P/S problems)
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -128,12 +134,35 @@ class Problem:
         return ((iz * self.ny + iy) * self.nx + ix).astype(np.int32), np.stack([wx, wy, wz], 1)
 
     @property
+    def obs_used(self):
+        """Observations the sampler fits (mceik_mcmc_init): used P picks, and used
+        S picks when the chains hold an S model."""
+        k = self.obs_stat
+        ok = (self.luse != 0) & (k >= 0) & (k < self.nstat)
+        sel = self.pick_type == P_PRIMARY_PICK
+        if self.nphase > 1:
+            sel = sel | (self.pick_type == S_PRIMARY_PICK)
+        return ok & sel
+
+    @property
     def obs_mask(self):
-        return (~((self.luse != 0) & (self.pick_type == P_PRIMARY_PICK))).astype(np.int32)
+        return (~self.obs_used).astype(np.int32)
+
+    @property
+    def obs_phase(self):
+        """0 = P, 1 = S: the model an observation is fit against."""
+        return (self.obs_used & (self.pick_type == S_PRIMARY_PICK)).astype(np.int32)
 
     @property
     def tcorr(self):
-        return np.where(self.obs_mask == 0, self.pcorr[self.obs_stat], 0.0)
+        sc = self.scorr if self.scorr is not None else np.zeros(self.nstat)
+        corr = np.where(self.obs_phase == 1, sc[self.obs_stat], self.pcorr[self.obs_stat])
+        return np.where(self.obs_mask == 0, corr, 0.0)
+
+    @property
+    def n_s_picks(self):
+        k = self.obs_stat
+        return int(((self.luse != 0) & (k >= 0) & (k < self.nstat) & (self.pick_type == S_PRIMARY_PICK)).sum())
 
     # --- mceik_struct.h views (ctypes), kept alive on the problem ---
     def structs(self):
@@ -164,9 +193,10 @@ class Problem:
         st.lcartesian = 1
         st.xrec, st.yrec, st.zrec = dp(self.sx), dp(self.sy), dp(self.sz)
         st.pcorr = dp(self.pcorr)
-        st.scorr = dp(np.zeros(self.nstat))
-        st.lhasP = ip(np.ones(self.nstat))
-        st.lhasS = ip(np.zeros(self.nstat))
+        st.scorr = dp(self.scorr if self.scorr is not None else np.zeros(self.nstat))
+        has = lambda t: np.array([((self.obs_stat == k) & (self.pick_type == t)).any() for k in range(self.nstat)])
+        st.lhasP = ip(has(P_PRIMARY_PICK))
+        st.lhasS = ip(has(S_PRIMARY_PICK))
         cat = _lib.CatalogStruct()
         cat.nevents = self.nevents
         cat.xsrc, cat.ysrc, cat.zsrc = dp(self.ex), dp(self.ey), dp(self.ez)
@@ -190,13 +220,18 @@ def cell_velocity(p: Problem):
 
 
 def make_problem(config="C3", n=None, nstat=None, nev=None, h=None, homogeneous=None, nref=(4, 4, 4),
-                 seed=2016, maxit=50, tol=1e-8, picks="analytic"):
+                 seed=2016, maxit=50, tol=1e-8, picks="analytic", phases="P"):
     """Synthetic problem of a BASELINE configuration (SURVEY s.8d).
 
     picks: 'analytic' -> straight-ray times in the mean velocity (no GPU needed);
-           a callable(problem) -> [nstat, nev] travel times, e.g. the GPU forward
-           of `v_true` (see `picks_from_forward`).  Gaussian noise (sigma 0.05 s)
-           is added, varObs = 0.25 s^2 (homog.c:55).
+           a callable(problem, phase) -> [nstat, nev] travel times in the P
+           (phase 0) or S (phase 1) model, e.g. the GPU forward of `v_true` /
+           `vs_true` (see `picks_from_forward`).  Gaussian noise (sigma 0.05 s)
+           is added, varObs = 0.25 s^2 (homog.c:55-56).
+    phases: 'P' (every station picks P of every event) or 'PS' (a P and an S
+           pick per station and event, in homog.c's order, homog.c:203-229;
+           the chains then hold a P and an S model, vs = vp / sqrt(3) as
+           homog.c:53-54).
     """
     cfg = dict(CONFIGS[config])
     n = n or cfg["n"]; nstat = nstat or cfg["nstat"]; nev = nev or cfg["nev"]
@@ -210,34 +245,54 @@ def make_problem(config="C3", n=None, nstat=None, nev=None, h=None, homogeneous=
     p.sy = rng.uniform(2 * h, ext - 2 * h, nstat)
     p.sz = np.full(nstat, ext)
     p.pcorr = np.zeros(nstat)
+    p.scorr = np.zeros(nstat)
     p.ex = rng.uniform(h, ext - h, nev)
     p.ey = rng.uniform(h, ext - h, nev)
     p.ez = rng.uniform(h, ext - h, nev)
     p.v_true = np.full(p.ncell, 2000 if config == "C1" else 4000, np.int32) if homogeneous else cell_velocity(p)
-    # every station sees every event (P only), CSR by event
-    p.obs_ptr = (np.arange(nev + 1) * nstat).astype(np.int32)
-    p.obs_stat = np.tile(np.arange(nstat, dtype=np.int32), nev)
-    p.pick_type = np.full(nev * nstat, P_PRIMARY_PICK, np.int32)
-    p.luse = np.ones(nev * nstat, np.int32)
-    p.var = np.full(nev * nstat, 0.25)
-    if picks == "analytic":
-        vmean = float(np.mean(p.v_true))
-        d = np.sqrt((p.sx[:, None] - p.ex[None]) ** 2 + (p.sy[:, None] - p.ey[None]) ** 2 +
-                    (p.sz[:, None] - p.ez[None]) ** 2)
-        tt = d / vmean                               # [nstat, nev]
-    else:
-        tt = np.asarray(picks(p), dtype=np.float64).reshape(nstat, nev)
-    p.tobs = (tt.T.ravel() + rng.normal(0.0, 0.05, nev * nstat)).astype(np.float64)
+    nph = 2 if phases == "PS" else 1
+    if phases not in ("P", "PS"):
+        raise ValueError(f"phases: 'P' or 'PS', not {phases!r}")
+    p.nphase = nph
+    if nph == 2:
+        p.vs_true = np.rint(p.v_true / np.sqrt(3.0)).astype(np.int32)
+    # every station sees every event, CSR by event; per station P (then S)
+    per = nstat * nph
+    p.obs_ptr = (np.arange(nev + 1) * per).astype(np.int32)
+    p.obs_stat = np.tile(np.repeat(np.arange(nstat, dtype=np.int32), nph), nev)
+    p.pick_type = np.tile(np.arange(1, nph + 1, dtype=np.int32), nev * nstat)
+    p.luse = np.ones(nev * per, np.int32)
+    p.var = np.full(nev * per, 0.25)
+    tt = np.empty((nph, nstat, nev))
+    for ph in range(nph):
+        if picks == "analytic":
+            vmean = float(np.mean(p.vs_true if ph else p.v_true))
+            d = np.sqrt((p.sx[:, None] - p.ex[None]) ** 2 + (p.sy[:, None] - p.ey[None]) ** 2 +
+                        (p.sz[:, None] - p.ez[None]) ** 2)
+            tt[ph] = d / vmean                           # [nstat, nev]
+        else:
+            tt[ph] = np.asarray(picks(p, ph) if nph == 2 else picks(p), dtype=np.float64).reshape(nstat, nev)
+    # observation (e, k, ph) at e*per + k*nph + ph
+    p.tobs = (tt.transpose(2, 1, 0).ravel() + rng.normal(0.0, 0.05, nev * per)).astype(np.float64)
     return p
 
 
 def initial_models(p: Problem, chain_ids, amp=50):
     """Per-chain start model: v_true + integer noise in [-amp, amp], keyed by the
-    GLOBAL chain id so the chains do not depend on how they are sharded."""
-    out = np.empty((len(chain_ids), p.ncell), np.int32)
+    GLOBAL chain id so the chains do not depend on how they are sharded.
+    [n, ncell] for P problems, [n, 2, ncell] (P, S) for P/S problems."""
+    if p.nphase == 1:
+        out = np.empty((len(chain_ids), p.ncell), np.int32)
+        for r, gid in enumerate(chain_ids):
+            g = np.random.default_rng([p.seed, int(gid)])
+            out[r] = np.clip(p.v_true + g.integers(-amp, amp + 1, p.ncell), p.vmin, p.vmax)
+        return out
+    out = np.empty((len(chain_ids), 2, p.ncell), np.int32)
     for r, gid in enumerate(chain_ids):
         g = np.random.default_rng([p.seed, int(gid)])
-        out[r] = np.clip(p.v_true + g.integers(-amp, amp + 1, p.ncell), p.vmin, p.vmax)
+        out[r, 0] = np.clip(p.v_true + g.integers(-amp, amp + 1, p.ncell), p.vmin, p.vmax)
+        g = np.random.default_rng([p.seed, int(gid), 1])
+        out[r, 1] = np.clip(p.vs_true + g.integers(-amp, amp + 1, p.ncell), p.vsmin, p.vsmax)
     return out
 
 
@@ -259,7 +314,7 @@ class Sampler:
         if v0 is None:
             v0 = initial_models(p, range(chain_offset, chain_offset + nchains))
         self.v0 = np.ascontiguousarray(v0, dtype=np.int32)
-        assert self.v0.shape == (self.nchains, p.ncell)
+        assert self.v0.shape == self.model_shape, (self.v0.shape, self.model_shape)
         L = _lib.lib()
         parms, st, cat = p.structs()
         o = _lib.McmcOpts()
@@ -269,6 +324,7 @@ class Sampler:
         o.max_samples, o.device = int(max_samples), int(device)
         o.precision, o.max_waves = int(precision), int(max_waves)
         o.tt_interp = int(p.tt_interp)
+        o.nphase, o.vsmin, o.vsmax, o.mask_s = int(p.nphase), int(p.vsmin), int(p.vsmax), int(p.mask_s)
         h = C.c_void_p()
         rc = L.mceik_mcmc_init(C.byref(parms), C.byref(st), C.byref(cat), C.byref(o),
                                self.v0.ctypes.data_as(C.c_void_p), C.byref(h))
@@ -277,6 +333,13 @@ class Sampler:
         self._h = h
         self._L = L
         self.max_samples = int(max_samples)
+        self._last_full = True          # the last forward solved every model (init / restore)
+
+    @property
+    def model_shape(self):
+        """Shape of the chains' models: [nchains, ncell] (P) or [nchains, 2, ncell] (P, S)."""
+        p = self.p
+        return (self.nchains, p.ncell) if p.nphase == 1 else (self.nchains, p.nphase, p.ncell)
 
     def set_stream(self, stream_ptr):
         self._L.mceik_mcmc_set_stream(self._h, C.c_void_p(stream_ptr))
@@ -285,12 +348,25 @@ class Sampler:
         rc = self._L.mceik_mcmc_run(self._h, int(nsteps))
         if rc != 0:
             raise RuntimeError(f"mceik_mcmc_run failed ({rc})")
+        if nsteps:
+            self._last_full = False
 
     def sync(self):
         self._L.mceik_mcmc_sync(self._h)
 
+    def info(self):
+        """mceik_mcmc_get_info as a dict (pipes, kernel instance, waves, workspaces)."""
+        i = _lib.McmcInfo()
+        if self._L.mceik_mcmc_get_info(self._h, C.byref(i)) != 0:
+            raise RuntimeError("mceik_mcmc_get_info failed")
+        n = i.npipe
+        return {"npipe": n, "nphase": i.nphase, "step_z": i.step_z, "fixed_layout": bool(i.fixed_layout),
+                "chains": list(i.chains[:n]), "waves": list(i.waves[:n]),
+                "workspace_bytes": list(i.workspace_bytes[:n]), "lds_bytes": int(i.lds_bytes),
+                "masked_s": i.masked_s, "kernel": i.kernel.decode()}
+
     def state(self):
-        v = np.empty((self.nchains, self.p.ncell), np.int32)
+        v = np.empty(self.model_shape, np.int32)
         logl = np.empty(self.nchains, np.float64)
         nacc = np.empty(self.nchains, np.int64)
         step = C.c_longlong(0)
@@ -301,14 +377,18 @@ class Sampler:
         return v, logl, nacc, step.value
 
     def last(self, with_ierr=False):
-        """Host copies of the last step's travel-time table, iteration counts and
-        accept flags (and the per-solve reference ierr if with_ierr)."""
+        """Host copies of the last forward's travel-time tables, iteration counts and
+        accept flags (and the per-solve reference ierr if with_ierr).  After a step:
+        [nchains, nstat, nev] / [nchains, nstat] of the model each proposal changed
+        (`last_phase`); after init / restore with two models: [nchains, 2, nstat, nev]
+        / [nchains, 2, nstat]."""
         tt, it, acc, ie = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
         self._L.mceik_mcmc_last(self._h, C.byref(tt), C.byref(it), C.byref(acc), C.byref(ie))
         p = self.p
-        ttab = np.empty((self.nchains, p.nstat, p.nevents), np.float32)
-        niter = np.empty((self.nchains, p.nstat), np.int32)
-        ierr = np.empty((self.nchains, p.nstat), np.int32)
+        mid = (p.nphase,) if (self._last_full and p.nphase > 1) else ()
+        ttab = np.empty((self.nchains,) + mid + (p.nstat, p.nevents), np.float32)
+        niter = np.empty((self.nchains,) + mid + (p.nstat,), np.int32)
+        ierr = np.empty((self.nchains,) + mid + (p.nstat,), np.int32)
         a = np.empty(self.nchains, np.uint8)
         self.sync()
         for dst, src in ((ttab, tt), (niter, it), (a, acc), (ierr, ie)):
@@ -316,11 +396,21 @@ class Sampler:
                 raise RuntimeError("mceik_memcpy failed")
         return (ttab, niter, a, ierr) if with_ierr else (ttab, niter, a)
 
+    def last_phase(self):
+        """The model each chain's last proposal changed (0 = P, 1 = S)."""
+        ph = C.c_void_p()
+        self._L.mceik_mcmc_last_phase(self._h, C.byref(ph))
+        out = np.empty(self.nchains, np.int32)
+        self.sync()
+        if self._L.mceik_memcpy(out.ctypes.data_as(C.c_void_p), ph, out.nbytes, 1) != 0:
+            raise RuntimeError("mceik_memcpy failed")
+        return out
+
     def checkpoint(self):
         """Complete chain state (mceik_mcmc_checkpoint): dict of v, logl, naccept,
         step, nkept -- restore() into a sampler of the same problem/shard resumes
         the chains bit for bit."""
-        v = np.empty((self.nchains, self.p.ncell), np.int32)
+        v = np.empty(self.model_shape, np.int32)
         logl = np.empty(self.nchains, np.float64)
         nacc = np.empty(self.nchains, np.int64)
         step, nkept = C.c_longlong(0), C.c_int(0)
@@ -335,7 +425,7 @@ class Sampler:
         if ck.get("chain_offset", self.chain_offset) != self.chain_offset or ck.get("seed", self.p.seed) != self.p.seed:
             raise ValueError("checkpoint belongs to another chain shard or seed")
         v = np.ascontiguousarray(ck["v"], dtype=np.int32)
-        assert v.shape == (self.nchains, self.p.ncell)
+        assert v.shape == self.model_shape
         logl = None if recompute_logl else np.ascontiguousarray(ck["logl"], dtype=np.float64)
         nacc = np.ascontiguousarray(ck["naccept"], dtype=np.int64)
         rc = self._L.mceik_mcmc_restore(self._h, v.ctypes.data_as(C.c_void_p),
@@ -343,6 +433,8 @@ class Sampler:
                                         nacc.ctypes.data_as(C.c_void_p), int(ck["step"]), int(ck.get("nkept", 0)))
         if rc != 0:
             raise RuntimeError(f"mceik_mcmc_restore failed ({rc})")
+        if recompute_logl:
+            self._last_full = True
 
     def fsm_stats(self, reset=False):
         """(FSM kernel ms from hipEvents, launches, executed iterations summed over
@@ -353,13 +445,13 @@ class Sampler:
         return ms.value, nl.value, it.value, tuple(tv)
 
     def samples(self, max_states=None, device_ptr=None):
-        """Kept states [k, nchains, ncell] (host numpy, or copied into device_ptr)."""
+        """Kept states [k, *model_shape] (host numpy, or copied into device_ptr)."""
         max_states = self.max_samples if max_states is None else max_states
         n = C.c_int(0)
         if device_ptr is not None:
             self._L.mceik_mcmc_get_samples(self._h, C.c_void_p(device_ptr), None, max_states, 1, C.byref(n))
             return n.value
-        v = np.empty((max(max_states, 1), self.nchains, self.p.ncell), np.int32)
+        v = np.empty((max(max_states, 1),) + self.model_shape, np.int32)
         lg = np.empty((max(max_states, 1), self.nchains), np.float64)
         self._L.mceik_mcmc_get_samples(self._h, v.ctypes.data_as(C.c_void_p), lg.ctypes.data_as(C.c_void_p),
                                        max_states, 0, C.byref(n))
@@ -380,14 +472,16 @@ class Sampler:
 def picks_from_forward(device=0, precision=64):
     """picks callable for make_problem: GPU forward of the true model (fp64 by
     default: the reference's arithmetic, and a different kernel instance from
-    the fp32 sampler so profiles of the two do not mix)."""
-    def f(p: Problem):
+    the fp32 sampler so profiles of the two do not mix).  f(p) or f(p, phase):
+    phase 1 solves the S model `vs_true`."""
+    def f(p: Problem, phase=0):
         import torch
         from .eikonal import BatchSolver
         dev = torch.device("cuda", device)
         bs = BatchSolver(p.nx, p.ny, p.nz, p.h, p.x0, p.y0, p.z0, p.maxit, p.tol, precision, nref=p.nref)
         src = torch.tensor(np.stack([np.zeros(p.nstat), p.sx, p.sy, p.sz], 1)[:, None, :], dtype=torch.float64)
-        slow = torch.tensor((1.0 / p.v_true.astype(np.float32)).astype(np.float32).reshape(1, -1), device=dev)
+        vt = p.vs_true if phase else p.v_true
+        slow = torch.tensor((1.0 / vt.astype(np.float32)).astype(np.float32).reshape(1, -1), device=dev)
         out = bs.solve(src, slow, ev_node=torch.tensor(p.ev_node))
         torch.cuda.synchronize(dev)
         return out["ttab"].cpu().numpy().reshape(p.nstat, p.nevents)
@@ -408,7 +502,7 @@ def gather_kept(smp: Sampler, nchains_total, group=None, dst=0, device=None):
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     width = -(-nchains_total // world)
-    ncell = smp.p.ncell
+    ncell = smp.p.ncell * smp.p.nphase           # a chain's model entries
     if device is not None:
         v = torch.zeros((width, ncell), dtype=torch.int32, device=device)
         lg = torch.zeros((width,), dtype=torch.float64, device=device)
@@ -423,7 +517,7 @@ def gather_kept(smp: Sampler, nchains_total, group=None, dst=0, device=None):
             raise RuntimeError("no kept state to gather (max_samples = 0 or still in burn-in)")
         v = torch.zeros((width, ncell), dtype=torch.int32)
         lg = torch.zeros((width,), dtype=torch.float64)
-        v[:smp.nchains] = torch.from_numpy(kv[0])
+        v[:smp.nchains] = torch.from_numpy(kv[0].reshape(smp.nchains, ncell))
         lg[:smp.nchains] = torch.from_numpy(kl[0])
     gv = [torch.empty_like(v) for _ in range(world)] if rank == dst else None
     gl = [torch.empty_like(lg) for _ in range(world)] if rank == dst else None
@@ -478,7 +572,7 @@ class Comm:
         root, (None, None) elsewhere."""
         is_root = self.rank == root
         if is_root and v_out is None:
-            v_out = np.empty((nchains_total, smp.p.ncell), np.int32)
+            v_out = np.empty((nchains_total,) + smp.model_shape[1:], np.int32)
             logl_out = np.empty(nchains_total, np.float64) if logl_out is None else logl_out
 
         def ptr(a):

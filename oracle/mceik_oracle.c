@@ -293,6 +293,9 @@ typedef struct {
     int vmin, vmax, dvmax;
     uint32_t seed;
     const float *ev_frac;         /* NULL, or trilinear mode: [nevents][3] fractions, ev_node = cell corner */
+    int nphase;                   /* velocity models per chain: 1 = P, 2 = P and S (homog.c:208-258) */
+    int vsmin, vsmax;             /* S prior (nphase 2) */
+    const int *obs_phase;         /* NULL (all P) or [nobs] 0 = P, 1 = S: the model an observation fits */
 } oracle_mcmc_problem;
 
 /* Travel time of an event from a solved fp32 field u (x fastest).  w == NULL:
@@ -358,24 +361,30 @@ int oracle_forward_f32(const oracle_mcmc_problem *p, const int *v, float *ttab, 
 }
 
 /* logL = -sum_e objfn_e, objfn_e = locate.c L2 with analytic t0 at the
- * event's node (one grid point, iwantOT = 1), observations in CSR order. */
+ * event's node (one grid point, iwantOT = 1), observations in CSR order.
+ * ttab [phase][station][event]: an observation of phase ph (obs_phase, P if
+ * NULL) is fit against model ph's table of its station -- the locator stacks
+ * P and S picks alike (locate.f90:399,442; the build's definition, DESIGN s.4). */
 double oracle_loglik(const oracle_mcmc_problem *p, const float *ttab)
 {
     double logl = 0.0;
     const double sqrt2i = 0.7071067811865475;
+    const size_t per = (size_t)p->nstat * p->nevents;
     for (int e = 0; e < p->nevents; e++) {
         int j0 = p->obs_ptr[e], j1 = p->obs_ptr[e + 1];
         double xnorm = 0.0, t0 = 0.0, obj = 0.0;
         for (int j = j0; j < j1; j++) if (!p->obs_mask[j]) xnorm = xnorm + 1.0 / p->var[j];
         for (int j = j0; j < j1; j++) {
             if (p->obs_mask[j]) continue;
-            double te = (double)ttab[(size_t)p->obs_stat[j] * p->nevents + e];
+            const int ph = p->obs_phase ? p->obs_phase[j] : 0;
+            double te = (double)ttab[ph * per + (size_t)p->obs_stat[j] * p->nevents + e];
             double tc = p->tobs[j] - p->tcorr[j];
             t0 = t0 + ((1.0 / p->var[j]) / xnorm) * (tc - te);
         }
         for (int j = j0; j < j1; j++) {
             if (p->obs_mask[j]) continue;
-            double te = (double)ttab[(size_t)p->obs_stat[j] * p->nevents + e];
+            const int ph = p->obs_phase ? p->obs_phase[j] : 0;
+            double te = (double)ttab[ph * per + (size_t)p->obs_stat[j] * p->nevents + e];
             double tc = p->tobs[j] - p->tcorr[j];
             double res = ((1.0 / p->var[j]) * sqrt2i) * (tc - (te + t0));
             obj = obj + res * res;
@@ -385,39 +394,57 @@ double oracle_loglik(const oracle_mcmc_problem *p, const float *ttab)
     return logl;
 }
 
+static int oracle_nphase(const oracle_mcmc_problem *p) { return p->nphase > 1 ? p->nphase : 1; }
+
+/* Proposal (build definition): one cell of the chain's nphase models, drawn
+ * over [0, nphase*ncell) (cell / ncell = the model: 0 P, 1 S), moves by
+ * +-[1, dvmax]; v is the chain's [nphase][ncell]. */
 void oracle_propose(const oracle_mcmc_problem *p, uint32_t chain, uint64_t step,
                     const int *v, int *cell, int *vnew, int *in_prior, double *logu)
 {
     uint32_t ctr[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0u, 0u}, key[2] = {chain, p->seed}, r[4];
     oracle_philox4x32_10(ctr, key, r);
     uint32_t ncell = (uint32_t)(p->ncx * p->ncy * p->ncz);
-    int c = (int)(((uint64_t)r[0] * ncell) >> 32);
+    uint32_t ncm = ncell * (uint32_t)oracle_nphase(p);
+    int c = (int)(((uint64_t)r[0] * ncm) >> 32);
     int mag = 1 + (int)(((uint64_t)r[1] * (uint32_t)p->dvmax) >> 32);
     int vn = v[c] + ((r[2] & 1u) ? -mag : mag);
+    int sph = c >= (int)ncell;
     *cell = c; *vnew = vn;
-    *in_prior = (vn >= p->vmin && vn <= p->vmax);
+    *in_prior = sph ? (vn >= p->vsmin && vn <= p->vsmax) : (vn >= p->vmin && vn <= p->vmax);
     *logu = oracle_det_log(((double)r[3] + 0.5) * (1.0 / 4294967296.0));
 }
 
+/* Tables [phase][station][event] of every model of one chain (v [nphase][ncell]). */
+int oracle_forward_all_f32(const oracle_mcmc_problem *p, const int *v, float *ttab)
+{
+    const size_t ncell = (size_t)p->ncx * p->ncy * p->ncz, per = (size_t)p->nstat * p->nevents;
+    int nerr = 0;
+    for (int ph = 0; ph < oracle_nphase(p); ph++) nerr += oracle_forward_f32(p, v + ph * ncell, ttab + ph * per, NULL);
+    return nerr;
+}
+
 /* Runs nsteps Metropolis steps for nchains chains (global ids gid0..); v is
- * [nchains][ncell] in/out, logl [nchains] in/out; accept [nsteps][nchains]. */
+ * [nchains][nphase][ncell] in/out, logl [nchains] in/out; accept
+ * [nsteps][nchains].  Every proposal's logL comes from a forward of all of
+ * the chain's models (the GPU re-solves only the changed one). */
 void oracle_mcmc_run(const oracle_mcmc_problem *p, int nchains, uint32_t gid0, uint64_t step0,
                      int nsteps, int *v, double *logl, unsigned char *accept, double *logl_trace)
 {
-    size_t ncell = (size_t)p->ncx * p->ncy * p->ncz;
-    int *vp = (int *)malloc(ncell * sizeof(int));
-    float *tt = (float *)malloc(sizeof(float) * p->nstat * p->nevents);
+    size_t ncm = (size_t)p->ncx * p->ncy * p->ncz * oracle_nphase(p);
+    int *vp = (int *)malloc(ncm * sizeof(int));
+    float *tt = (float *)malloc(sizeof(float) * p->nstat * p->nevents * oracle_nphase(p));
     for (int st = 0; st < nsteps; st++) {
         for (int c = 0; c < nchains; c++) {
-            int *vc = v + (size_t)c * ncell;
+            int *vc = v + (size_t)c * ncm;
             int cell, vn, inp;
             double logu;
             oracle_propose(p, gid0 + (uint32_t)c, step0 + (uint64_t)st, vc, &cell, &vn, &inp, &logu);
             double ln = -HUGE_VAL;
             if (inp) {          /* outside the prior: rejected without a forward */
-                memcpy(vp, vc, ncell * sizeof(int));
+                memcpy(vp, vc, ncm * sizeof(int));
                 vp[cell] = vn;
-                oracle_forward_f32(p, vp, tt, NULL);
+                oracle_forward_all_f32(p, vp, tt);
                 ln = oracle_loglik(p, tt);
             }
             int acc = inp && (logu < ln - logl[c]);

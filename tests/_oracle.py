@@ -128,7 +128,8 @@ class McmcProblem(C.Structure):
                [(n, C.c_void_p) for n in ("sx", "sy", "sz", "ev_node", "obs_ptr", "obs_stat", "obs_mask",
                                           "tobs", "tcorr", "var")] + \
                [("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int), ("seed", C.c_uint32),
-                ("ev_frac", C.c_void_p)]
+                ("ev_frac", C.c_void_p), ("nphase", C.c_int), ("vsmin", C.c_int), ("vsmax", C.c_int),
+                ("obs_phase", C.c_void_p)]
 
 
 def make_problem(pb):
@@ -140,6 +141,8 @@ def make_problem(pb):
     for n in ("h", "x0", "y0", "z0", "tol"):
         setattr(P, n, float(getattr(pb, n)))
     P.seed = int(pb.seed)
+    P.nphase = int(getattr(pb, "nphase", 1))
+    P.vsmin, P.vsmax = int(getattr(pb, "vsmin", 0)), int(getattr(pb, "vsmax", 0))
     keep = []
     interp = bool(getattr(pb, "tt_interp", 0))
     ev_node, ev_frac = pb.ev_cell if interp else (pb.ev_node, None)
@@ -154,6 +157,10 @@ def make_problem(pb):
         a = np.ascontiguousarray(ev_frac, dtype=np.float32)
         keep.append(a)
         P.ev_frac = a.ctypes.data
+    if P.nphase > 1:
+        a = np.ascontiguousarray(pb.obs_phase, dtype=np.int32)
+        keep.append(a)
+        P.obs_phase = a.ctypes.data
     P._keep = keep
     return P
 
@@ -177,14 +184,33 @@ def event_time(u, nx, ny, nz, node, w=None):
 
 
 def loglik(P, tt):
+    """tt [nstat][nev] (P only) or [nphase][nstat][nev]."""
     tt = np.ascontiguousarray(tt, dtype=np.float32)
     return lib().oracle_loglik(C.byref(P), _p(tt))
+
+
+def forward_all_f32(P, v):
+    """Tables [nphase][nstat][nev] of every model of one chain (v [nphase*ncell])."""
+    nph = max(1, int(P.nphase))
+    tt = np.zeros(nph * P.nstat * P.nevents, dtype=np.float32)
+    v = np.ascontiguousarray(v, dtype=np.int32)
+    lib().oracle_forward_all_f32(C.byref(P), _p(v), _p(tt))
+    return tt.reshape(nph, P.nstat, P.nevents)
+
+
+def propose(P, chain, step, v):
+    """oracle_propose: (cell over the chain's [nphase][ncell] entries, new v, in prior, log U)."""
+    cell, vn, inp, logu = C.c_int(0), C.c_int(0), C.c_int(0), C.c_double(0.0)
+    v = np.ascontiguousarray(v, dtype=np.int32)
+    lib().oracle_propose(C.byref(P), C.c_uint32(chain), C.c_uint64(step), _p(v), C.byref(cell), C.byref(vn),
+                         C.byref(inp), C.byref(logu))
+    return cell.value, vn.value, bool(inp.value), logu.value
 
 
 def mcmc_run(P, v, logl, gid0, step0, nsteps):
     v = np.ascontiguousarray(v, dtype=np.int32).copy()
     logl = np.ascontiguousarray(logl, dtype=np.float64).copy()
-    nch = v.shape[0]
+    nch = v.shape[0]        # v [nchains][ncell] or [nchains][nphase][ncell]
     acc = np.zeros((nsteps, nch), dtype=np.uint8)
     trace = np.zeros((nsteps, nch), dtype=np.float64)
     lib().oracle_mcmc_run(C.byref(P), nch, gid0, step0, nsteps, _p(v), _p(logl), _p(acc), _p(trace))

@@ -109,6 +109,7 @@ def _offsets_c(header, ctype, fields):
     ("mceik_eikonal.h", "mceik_fsm_batch", "FsmBatch"),
     ("mceik_eikonal.h", "mceik_relocate_batch", "RelocateBatch"),
     ("mceik.h", "mceik_mcmc_opts", "McmcOpts"),
+    ("mceik.h", "mceik_mcmc_info", "McmcInfo"),
 ])
 def test_ctypes_batch_structs_match_public_headers(header, ctype, pyname):
     """Every field of the ctypes mirrors sits at the C offset (the batch

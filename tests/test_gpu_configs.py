@@ -7,12 +7,15 @@ oracle_mcmc_run) bit for bit:
 * C1  1 chain, 32^3 homogeneous, 4 stations, 100 proposals (the plumbing case)
 * C2  256 chains x 16 stations at 64^3: 4096 solves on at most 2048 waves,
       so waves run several solves in their reused scratch field
-* C3  128^3, 32 stations, 32 events: the bench's instance
-      fsm_solve_kernel<float, 2, true, 2, 1, 4> (cells, LDS cell cache, short
-      sqrt, compile-time kb = 4, 1024 z-blocks = MCEIK_MAX_BLOCKS), with fewer
-      resident waves than solves; then two MCMC steps
-* C5  256^3 (8 x 8 x 8-brick columns: the runtime-kb kernel with 32-brick
-      z-blocks), two full fields
+* C3  128^3, 32 stations, 32 events: the bench's own production launch --
+      1024 chains in two pipes, fsm16_solve_kernel<2, 1> (16-z steps, the
+      fixed LDS layout, cell cache, short sqrt) on 2 x 2048 resident waves in
+      two workspaces -- with chains on both sides of the pipe split checked
+      after init and one step; plus 4 chains on 16 waves (8 solves per wave in
+      reused scratch) and two MCMC steps
+* C5  256^3, 64 stations: the sampler's own launch (fsm16_solve_kernel<0, 4>,
+      32-brick z-blocks, scratch-budget-capped waves, several solves per
+      wave) checked on one chain; and two full fields
 C4 is C3's geometry sharded over 8 GPUs (the driver's scaling run).
 The CPU side uses the oracle's OpenMP (one solve per thread).
 """
@@ -58,6 +61,71 @@ def test_c3_sampler_forward_bitwise_reused_scratch():
         assert np.array_equal(ttab[c].view(np.uint32), tt.view(np.uint32)), c
         assert np.array_equal(niter[c], it), c
         assert logl0[c] == O.loglik(P, tt)
+
+
+@pytest.mark.timeout(600)
+def test_c3_bench_production_launch_bitwise():
+    """The bench's exact C3 launch: Sampler(C3) with 1024 chains and the
+    library defaults (two pipes, occupancy-many waves, two workspaces).
+    Chains {0, 1, 511, 512, 1022, 1023} straddle the pipe split: their init
+    tables, iteration counts and logL == the fp32 twin, and their models and
+    logL after one step == oracle_mcmc_run."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("C3")
+    p.dvmax = 400
+    p.var[:] = 1e-6
+    s = mcmc.Sampler(p, nchains=1024)
+    info = s.info()
+    assert info["npipe"] == 2 and info["chains"] == [512, 512]
+    assert info["step_z"] == 16 and info["fixed_layout"]
+    assert info["kernel"] == "fsm16_solve_kernel<2, 1>"
+    assert min(info["waves"]) >= 1024, info           # the full-occupancy launch (2048 on a 256-CU MI355X)
+    v0, logl0, _, _ = s.state()
+    ttab, niter, _, ierr = s.last(with_ierr=True)
+    assert not ierr.any()
+    s.run(1)
+    v1, logl1, _, step = s.state()
+    _, nl, _, _ = s.fsm_stats()
+    s.close()
+    assert step == 1 and nl == 2                      # one timed half launch per pipe
+    P = O.make_problem(p)
+    chains = (0, 1, 511, 512, 1022, 1023)
+    for c in chains:
+        tt, it = O.forward_f32(P, v0[c])
+        assert np.array_equal(ttab[c].view(np.uint32), tt.view(np.uint32)), c
+        assert np.array_equal(niter[c], it), c
+        assert logl0[c] == O.loglik(P, tt), c
+        vo, lo, _, _ = O.mcmc_run(P, v0[c:c + 1], logl0[c:c + 1], c, 0, 1)
+        assert np.array_equal(v1[c], vo[0]), c
+        assert logl1[c].view(np.uint64) == lo[0].view(np.uint64), c
+
+
+@pytest.mark.timeout(600)
+def test_c5_sampler_launch_bitwise():
+    """C5 through the sampler: 256^3, 64 stations, 32 chains = 2048 solves per
+    step on scratch-budget-capped waves (the runtime-kb fsm16 instance with
+    32-brick z-blocks, each wave running several solves in its reused 128-MiB
+    u / u0 fields).  Chain 0's init tables of 8 stations == the fp32 twin."""
+    dev = _dev()
+    torch.cuda.empty_cache()
+    from mceik_amd import mcmc
+    p = mcmc.make_problem("C5", picks="analytic")
+    assert (p.nx, p.nstat, p.nevents) == (256, 64, 64)
+    s = mcmc.Sampler(p, nchains=32)
+    info = s.info()
+    v0, _, _, _ = s.state()
+    ttab, niter, _, ierr = s.last(with_ierr=True)
+    s.run(1)                                          # a step of the same launch runs too
+    s.close()
+    assert info["step_z"] == 16 and info["kernel"] == "fsm16_solve_kernel<0, 4>", info
+    assert sum(info["waves"]) < 32 * 64, info        # fewer resident waves than solves
+    assert not ierr.any()
+    P = O.make_problem(p)
+    P.nstat = 8                                       # the first 8 stations (same arrays)
+    tt, it = O.forward_f32(P, v0[0])
+    assert np.array_equal(ttab[0, :8].view(np.uint32), tt.view(np.uint32))
+    assert np.array_equal(niter[0, :8], it)
 
 
 def test_c3_mcmc_two_steps_bitwise():

@@ -382,6 +382,44 @@ def test_relocate_single_pass_c3_catalogue():
     assert torch.equal(ta.view(torch.int32), tb.view(torch.int32))
 
 
+@pytest.mark.parametrize("bad", ["nobs_short", "row_past_nrows"])
+def test_relocate_single_pass_rejects_a_broken_contract(bad):
+    """The single-pass kernel sizes its LDS from the caller's nobs / nrows: a
+    caller whose ev_ptr[nev] != nobs or whose obs_row reaches past nrows gets
+    NaN everywhere (no out-of-bounds LDS, no plausible misfits); the honest
+    description of the same batch gives finite values."""
+    import ctypes as C
+    from mceik_amd import _lib
+    dev = _dev()
+    nrows, ld, nev = 6, 1024, 3
+    tables = torch.rand((nrows, ld), device=dev)
+    ptr = [0, 4, 9, 12]
+    rows = [0, 1, 2, 3, 1, 2, 3, 4, 5, 0, 5, 2]
+    nobs = len(rows)
+    t = lambda a, dt: torch.tensor(np.asarray(a, dtype=dt), device=dev)
+    d_ptr, d_rows = t(ptr, np.int32), t(rows, np.int32)
+    d_tc, d_wt = t(np.linspace(1, 2, nobs), np.float32), t(np.ones(nobs), np.float32)
+    d_xn = t([4.0, 5.0, 3.0], np.float32)
+    out = torch.zeros((nev, ld), device=dev)
+    t0 = torch.zeros((nev, ld), device=dev)
+
+    def run(nr, no):
+        b = _lib.RelocateBatch()
+        b.ldgrd, b.ngrd, b.nev, b.iwantOT, b.t0use = ld, ld, nev, 1, 0.0
+        b.tables, b.ev_ptr, b.obs_row = tables.data_ptr(), d_ptr.data_ptr(), d_rows.data_ptr()
+        b.tc, b.wt, b.xnorm = d_tc.data_ptr(), d_wt.data_ptr(), d_xn.data_ptr()
+        b.t0, b.out, b.log_pdf = t0.data_ptr(), out.data_ptr(), 1
+        b.nrows, b.nobs = nr, no
+        assert _lib.lib().mceik_relocate(C.byref(b), C.c_void_p(0)) == 0
+        torch.cuda.synchronize(dev)
+        return out.clone(), t0.clone()
+
+    good, _ = run(nrows, nobs)
+    assert torch.isfinite(good).all()
+    o, z = run(nrows, nobs - 3) if bad == "nobs_short" else run(nrows - 2, nobs)
+    assert torch.isnan(o).all() and torch.isnan(z).all()
+
+
 def test_batch_solve_captured_in_a_graph_bitwise():
     """mceik_fsm_batch_solve only enqueues work (no allocation, no host sync;
     include/mceik_eikonal.h): captured once in a HIP graph (torch.cuda.graph)
