@@ -97,7 +97,8 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_b
            "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize", "mceik_mcmc_last_phase",
            "mceik_mcmc_get_info",
            "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write",
-           "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather")
+           "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather",
+           "os_path_exists", "os_path_isdir", "os_path_isfile", "os_makedirs", "os_mkdir")
 
 
 def lib():

@@ -682,73 +682,111 @@ static int blocks_solve(SingleState &S, int nsrc, const double *ts, const double
     return ierr_bc ? 1 : ierr;
 }
 
+// MPI of the calling process, resolved at run time (csrc/mpi_rt.c): -1 = the
+// caller runs no MPI (a single process: rank 0 of one).
+extern "C" int mceik_mpi_rank(int fcomm);
+extern "C" int mceik_mpi_bcast_int(int fcomm, int *v, int n, int root);
+extern "C" int mceik_mpi_bcast_double(int fcomm, double *v, int n, int root);
+
+// The MPI variant is collective over comm as the reference's
+// (fsm3d.f90:1583-1929): the master (rank 0) broadcasts its parameters at
+// initialize (:1626-1639) and its error at solve (:1792) and every rank
+// returns it.  One GPU holds the whole grid, so the master alone solves; the
+// other ranks take part in the broadcasts and keep their u untouched.  A
+// process without MPI is the master of one rank, except that a call passing
+// n < nx*ny*nz to solve acts as a non-master rank (the reference's callers
+// pass n = 1 there, fsm3d.f90:2102-2106) and returns ierr = 0.
+static int mpi_variant_rank(const int *comm) { return comm ? mceik_mpi_rank(*comm) : -1; }
+
 extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const int *nx, const int *ny, const int *nz,
                                      const int *ndivx, const int *ndivy, const int *ndivz, const int *noverlap,
                                      const int *maxit, const double *x0, const double *y0, const double *z0,
                                      const double *h, const double *tol, int *ierr)
 {
-    (void)comm;
     SingleState &S = g_single[2];
     *ierr = 0;
-    if (*iverb > 0) printf(" eikonal3d_initialize: Broadcasting parameters...\n");
-    if (*ndivx < 1 || *ndivy < 1 || *ndivz < 1 || *noverlap < 0) {
-        printf(" eikonal3d_initialize: Error computing local domain\n");
+    const int rank = mpi_variant_rank(comm);
+    // the master's parameters on every rank
+    int ip[9] = {*iverb, *nx, *ny, *nz, *ndivx, *ndivy, *ndivz, *noverlap, *maxit};
+    double dp[5] = {*x0, *y0, *z0, *h, *tol};
+    if (rank >= 0 && (mceik_mpi_bcast_int(*comm, ip, 9, 0) || mceik_mpi_bcast_double(*comm, dp, 5, 0))) {
+        printf(" eikonal3d_initialize: Error broadcasting parameters\n");
         *ierr = 1;
         return;
     }
-    if (single_alloc(S, 1, *nx, *ny, *nz, *maxit, 1)) {
-        printf(" eikonal3d_initialize: Error making the device structures\n");
+    if (ip[0] > 0 && rank <= 0) printf(" eikonal3d_initialize: Broadcasting parameters...\n");
+    int e = 0;
+    if (ip[4] < 1 || ip[5] < 1 || ip[6] < 1 || ip[7] < 0) {
+        if (rank <= 0) printf(" eikonal3d_initialize: Error computing local domain\n");
+        e = 1;
+    }
+    const int nd[3] = {ip[4], ip[5], ip[6]}, nn[3] = {ip[1], ip[2], ip[3]};
+    if (!e && rank <= 0) {            // the grid lives on the master's GPU
+        if (single_alloc(S, 1, nn[0], nn[1], nn[2], ip[8], 1)) e = 2;
+        for (int a = 0; a < 3 && !e; a++) {
+            S.D.nd[a] = nd[a];
+            S.D.step[a] = nn[a] / nd[a] > 1 ? nn[a] / nd[a] : 1;       // fsm3d.f90:1086-1088
+        }
+        S.D.nov = ip[7];
+        if (!e && nd[0] * nd[1] * nd[2] > 1 && blocks_buffers(S)) e = 2;
+        if (e == 2) printf(" eikonal3d_initialize: Error making the device structures\n");
+    }
+    // a failure on the master's device is every rank's failure
+    if (rank >= 0 && mceik_mpi_bcast_int(*comm, &e, 1, 0)) e = 1;
+    if (e) {
         *ierr = 1;
         return;
     }
-    const int nd[3] = {*ndivx, *ndivy, *ndivz}, nn[3] = {*nx, *ny, *nz};
-    for (int a = 0; a < 3; a++) {
-        S.D.nd[a] = nd[a];
-        S.D.step[a] = nn[a] / nd[a] > 1 ? nn[a] / nd[a] : 1;       // fsm3d.f90:1086-1088
-    }
-    S.D.nov = *noverlap;
-    if (nd[0] * nd[1] * nd[2] > 1 && blocks_buffers(S)) {
-        printf(" eikonal3d_initialize: Error making the device structures\n");
-        *ierr = 1;
-        return;
-    }
-    S.iverb = *iverb; S.maxit = *maxit; S.x0 = *x0; S.y0 = *y0; S.z0 = *z0; S.h = *h; S.tol = *tol;
+    S.nx = nn[0]; S.ny = nn[1]; S.nz = nn[2];
+    S.iverb = ip[0]; S.maxit = ip[8]; S.x0 = dp[0]; S.y0 = dp[1]; S.z0 = dp[2]; S.h = dp[3]; S.tol = dp[4];
     S.init = 1;
 }
 
 extern "C" void eikonal3d_solve(const int *comm, const int *nsrc, const int *n, const double *ts, const double *xs,
                                 const double *ys, const double *zs, const double *slow, double *u, int *ierr)
 {
-    (void)comm;
     SingleState &S = g_single[2];
     *ierr = 0;
+    const int rank = mpi_variant_rank(comm);
     if (!S.init) {
         printf(" eikonal3d_solve: solver not initialized\n");
         *ierr = 1;
         return;
     }
-    if ((long)*n < (long)S.nx * S.ny * S.nz) return;          // not the master: nothing to hold
-    const bool blocks = S.D.nd[0] * S.D.nd[1] * S.D.nd[2] > 1;
-    if (*nsrc < 1 || single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, *nsrc) || (blocks && blocks_buffers(S))) {
-        printf(" eikonal3d_solve: Error setting bcs\n");
-        *ierr = 1;
-        return;
+    int e = 0;
+    const bool master = rank == 0 || (rank < 0 && (long)*n >= (long)S.nx * S.ny * S.nz);
+    if (master) {
+        const bool blocks = S.D.nd[0] * S.D.nd[1] * S.D.nd[2] > 1;
+        if (*nsrc < 1 || (long)*n < (long)S.nx * S.ny * S.nz || single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, *nsrc) ||
+            (blocks && blocks_buffers(S))) {
+            printf(" eikonal3d_solve: Error setting bcs\n");
+            e = 1;
+        } else {
+            if (S.iverb > 0) printf(" eikonal3d_solve: Setting boundary conditions...\n");
+            const int rc = blocks ? blocks_solve(S, *nsrc, ts, xs, ys, zs, slow, u, nullptr)
+                                  : single_solve(S, S.maxit, *nsrc, S.tol, S.h, S.x0, S.y0, S.z0, ts, xs, ys, zs,
+                                                 slow, u, nullptr);
+            if (S.bcfail) printf(" eikonal3d_solve: Error setting bcs\n");
+            else if (rc != 0) printf(" eikonal3d_solve: Error calling solver\n");
+            e = rc < 0 ? 1 : rc;
+        }
     }
-    if (S.iverb > 0) printf(" eikonal3d_solve: Setting boundary conditions...\n");
-    const int rc = blocks ? blocks_solve(S, *nsrc, ts, xs, ys, zs, slow, u, nullptr)
-                          : single_solve(S, S.maxit, *nsrc, S.tol, S.h, S.x0, S.y0, S.z0, ts, xs, ys, zs, slow, u,
-                                         nullptr);
-    if (S.bcfail) printf(" eikonal3d_solve: Error setting bcs\n");
-    else if (rc != 0) printf(" eikonal3d_solve: Error calling solver\n");
-    *ierr = rc < 0 ? 1 : rc;
+    // the master's error on every rank (fsm3d.f90:1792)
+    if (rank >= 0 && mceik_mpi_bcast_int(*comm, &e, 1, 0)) e = 1;
+    *ierr = e;
 }
 
 extern "C" void eikonal3d_finalize(const int *comm, int *ierr)
 {
-    (void)comm;
-    single_free(g_single[2]);
-    g_single[2].init = 0;
+    SingleState &S = g_single[2];
     *ierr = 0;
+    if (!S.init) {                       // fsm3d.f90:1913-1916
+        printf(" eikonal3d_finalize: Solver was never initialized\n");
+        *ierr = 1;
+    }
+    if (mpi_variant_rank(comm) <= 0 && S.iverb > 0) printf(" eikonal3d_finalize: Freeing memory...\n");
+    single_free(S);
+    S.init = 0;
 }
 
 // ---------------------------------------------------------------------------

@@ -16,10 +16,10 @@ REF_INC = "/root/reference/include"
 
 def _declared_functions():
     names = set()
-    for h in ("mceik.h", "mceik_eikonal.h"):
+    for h in ("mceik.h", "mceik_eikonal.h", "os.h"):
         txt = open(os.path.join(INC, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-        for m in re.finditer(r"^\s*(?:int|void|size_t|double)\s+\**\s*([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
+        for m in re.finditer(r"^\s*(?:int|void|size_t|double|bool)\s+\**\s*([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
             names.add(m.group(1))
     return names
 
@@ -35,6 +35,28 @@ def test_library_loads_and_exports_every_declared_symbol():
     for name in declared:
         assert name in exported, name
         assert getattr(L, name) is not None
+
+
+def test_os_helpers(tmp_path):
+    """include/os.h (the reference's os.h, declared by its mceik.h): path tests,
+    mkdir, and makedirs of nested, existing and trailing-slash paths."""
+    from mceik_amd import _lib
+    L = _lib.lib()
+    for f in ("os_path_exists", "os_path_isdir", "os_path_isfile"):
+        getattr(L, f).restype = C.c_bool
+        getattr(L, f).argtypes = [C.c_char_p]
+    L.os_makedirs.argtypes = L.os_mkdir.argtypes = [C.c_char_p]
+    d = str(tmp_path).encode()
+    f = os.path.join(str(tmp_path), "a.txt")
+    open(f, "w").write("x")
+    assert L.os_path_isdir(d) and not L.os_path_isfile(d) and L.os_path_exists(d)
+    assert L.os_path_isfile(f.encode()) and not L.os_path_isdir(f.encode())
+    assert not L.os_path_exists(d + b"/nope") and not L.os_path_isdir(b"") and not L.os_path_isdir(None)
+    assert L.os_mkdir(d + b"/m") == 0 and L.os_path_isdir(d + b"/m")
+    assert L.os_mkdir(d + b"/m") == -1 and L.os_mkdir(d + b"/x/y") == -1
+    assert L.os_makedirs(d + b"/p/q/r") == 0 and L.os_path_isdir(d + b"/p/q/r")
+    assert L.os_makedirs(d + b"/p/q/r") == 0 and L.os_makedirs(d + b"/s/t/") == 0 and L.os_path_isdir(d + b"/s/t")
+    assert L.os_makedirs(f.encode() + b"/z") == -1 and L.os_makedirs(b"") == -1
 
 
 def test_missing_library_fails_loudly(monkeypatch):

@@ -104,8 +104,42 @@ def test_mpi_variant_from_c_caller(tmp_path):
     lines = {ln.split()[0]: ln.split() for ln in out.stdout.splitlines() if ln.strip()}
     assert float(lines["mpi_variant"][4]) == 1.4308203212738235
     assert float(lines["mpi_variant"][2]) == 0.0
+    # without MPI in the process, a call with n < nx*ny*nz acts as a non-master rank
     assert lines["non_master"][2] == "0" and float(lines["non_master"][4]) == -1.0
     assert float(lines["serial_driver"][4]) == 1.4308203212738235
+
+
+def test_mpi_variant_collective_contract_two_ranks(tmp_path):
+    """tests/c/xfsm3d_mpi.c under mpiexec -n 2: rank 0's parameters reach every
+    rank (rank 1 passes nonsense, fsm3d.f90:1626-1639); rank 0's SETBCS error
+    (source on the first node) is every rank's ierr (:1792); the solve gives
+    xfsm3d's known answer on rank 0 and leaves rank 1's u alone; finalizing
+    twice reports the reference's ierr = 1 (:1913-1916) on every rank."""
+    _dev()
+    mpi = "/opt/conda"
+    if not (os.path.exists(f"{mpi}/bin/mpiexec") and os.path.exists(f"{mpi}/lib/libmpi.so")):
+        pytest.skip("no MPI toolchain in this image")
+    exe = str(tmp_path / "xfsm3d_mpi")
+    lib = os.path.join(ROOT, "mceik_amd")
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), "-I", f"{mpi}/include",
+                    os.path.join(ROOT, "tests", "c", "xfsm3d_mpi.c"), "-L", lib, "-lmceik_hip",
+                    f"{mpi}/lib/libmpi.so", f"-Wl,-rpath,/usr/lib/x86_64-linux-gnu:{lib}:{mpi}/lib", "-lm",
+                    "-o", exe], check=True)
+    out = subprocess.run([f"{mpi}/bin/mpiexec", "-n", "2", exe], capture_output=True, text=True, timeout=120)
+    print(out.stdout, out.stderr[-2000:])
+    assert out.returncode == 0, out.stdout + out.stderr
+    got = {}
+    for ln in out.stdout.splitlines():
+        w = ln.split()
+        if len(w) >= 5 and w[1] == "rank":
+            got[(w[0], int(w[2]))] = w
+    for r in (0, 1):
+        assert got[("init", r)][4] == "0"
+        assert got[("origin", r)][4] == "1", r          # the master's SETBCS error on every rank
+        assert got[("solve", r)][4] == "0", r
+        assert got[("finalize", r)][4] == "0" and got[("refinalize", r)][4] == "1", r
+    assert float(got[("solve", 0)][6]) == 1.4308203212738235     # xfsm3d's known answer
+    assert float(got[("solve", 1)][6]) == -1.0                   # rank 1 holds no field
 
 
 @pytest.mark.parametrize("prec", [64, 32])
