@@ -116,6 +116,13 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
     lds_w4(x + XROW16(arr, 2 * h + 1, row), v[4], v[5], v[6], v[7]);
 }
 
+#ifndef MCEIK16_FULLLINE
+#define MCEIK16_FULLLINE 1       // the fixed instance (2-step positions) loads whole own lines
+#endif
+#ifndef MCEIK16_NPASS
+#define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
+#endif
+
 // ---- global loads / stores of 64-B segments ------------------------------
 // Pair-coalesced (lanes 2i, 2i+1 = x neighbours): each instruction makes both
 // lanes of a pair read the same line, so it touches 32 lines instead of 64.
@@ -198,6 +205,55 @@ __device__ __forceinline__ void raw_read(const float *x, int pb, float (&a)[16])
     lds_r4(x + pb + 4, a[8], a[9], a[10], a[11]);
     lds_r4(x + pb + 2 * XQE + 4, a[12], a[13], a[14], a[15]);
 }
+// ---- full-line own loads (FL: positions of 2 steps = one 128-B line per column)
+// A lane's position covers its column's whole 128-B line (two 16-z bricks);
+// x-adjacent lanes (a pair) run one step apart, so at every step exactly one
+// lane of a pair -- the "loader", whose prefetch target is the first brick of
+// its position -- needs a new line, and the other lane's target is the second
+// brick of the line its partner... of the line it loaded itself one step
+// earlier.  Both lanes of the pair load the loader's whole line in 4
+// instructions (lane parity p: quarters p and p+2 of each half, so an
+// instruction touches 32 lines, 32 B of each): the first half goes to the
+// loader's next-brick row at the end of the step, the second half is held in
+// registers for one step and then goes to the (then) non-loader's row.  Every
+// line is fetched once per visit instead of in two 64-B halves a step apart,
+// which the L2 re-fetched between the halves.
+struct LineLd {
+    float a[8];                  // now half: quarters p, p+2 of the loader's line
+    float h[8];                  // later half: quarters p, p+2 (held one step)
+    int rowl, rowo;              // XN rows: the loader's, the other lane's
+};
+__device__ __forceinline__ void line_issue(Rsrc r, uint32_t seg, bool isl, LineLd &q)
+{
+    const int lane = threadIdx.x, par = lane & 1;
+    const bool islp = dpp_swap_pair((unsigned)isl) != 0u;
+    const uint32_t segp = dpp_swap_pair(seg);
+    const uint32_t sl = isl ? seg : (islp ? segp : OOB);       // the loader's now-half segment
+    const uint32_t o = (uint32_t)par * 16u;
+    float t[4];
+    bload4(r, sl + o, t);
+    q.a[0] = t[0]; q.a[1] = t[1]; q.a[2] = t[2]; q.a[3] = t[3];
+    bload4(r, sl + o + 32u, t);
+    q.a[4] = t[0]; q.a[5] = t[1]; q.a[6] = t[2]; q.a[7] = t[3];
+    const uint32_t sh = sl ^ 64u;                               // the other half of the line (OOB stays OOB)
+    bload4(r, sh + o, t);
+    q.h[0] = t[0]; q.h[1] = t[1]; q.h[2] = t[2]; q.h[3] = t[3];
+    bload4(r, sh + o + 32u, t);
+    q.h[4] = t[0]; q.h[5] = t[1]; q.h[6] = t[2]; q.h[7] = t[3];
+    q.rowl = isl ? lane : (lane ^ 1);
+    q.rowo = lane ^ (q.rowl == lane ? 1 : 0);
+}
+// end of step: the loader's next brick (this step's now half) and the other
+// lane's (the half held since the previous step) into the XN rows
+__device__ __forceinline__ void line_write(float *x, const LineLd &q, const float (&hp)[8])
+{
+    const int par = threadIdx.x & 1;
+    lds_w4(x + XROW16(1, par, q.rowl), q.a[0], q.a[1], q.a[2], q.a[3]);
+    lds_w4(x + XROW16(1, par + 2, q.rowl), q.a[4], q.a[5], q.a[6], q.a[7]);
+    lds_w4(x + XROW16(1, par, q.rowo), hp[0], hp[1], hp[2], hp[3]);
+    lds_w4(x + XROW16(1, par + 2, q.rowo), hp[4], hp[5], hp[6], hp[7]);
+}
+
 // paired write-back of changed segments from raw_read operands t
 __device__ __forceinline__ void raw_store(Rsrc r, uint32_t seg, bool chg, const float (&t)[16])
 {
@@ -255,10 +311,22 @@ __device__ __forceinline__ void bload4h(Rsrc r, uint32_t off, float (&v)[4])
     f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MCEIK_HALO_AUX));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
+// Brick info of one lane's brick, packed (b0 / b1 ride two steps in VGPRs):
+// w1 = flags (12 bits) | zb << 12 (8) | ring slot << 20; w2 = cell-cache base
+// (signed 16) | position clock << 16; w3 = block id | BC z-slot mask << 16.
 struct BInfo16 {
     uint32_t seg;            // own 64-B segment (OOB if none)
     uint32_t zh;             // z-upwind node of a run start (prefetch only)
-    int zb, fl, ccb, ri, bid, clk, bcm;
+    uint32_t lseg;           // this brick's half of its column line if the line holds a valid brick
+                             // (prefetch only: a line loader whose own brick is past the grid end)
+    uint32_t w1, w2, w3;
+    __device__ __forceinline__ int fl() const { return (int)(w1 & 0xfffu); }
+    __device__ __forceinline__ int zb() const { return (int)((w1 >> 12) & 0xffu); }
+    __device__ __forceinline__ int ri() const { return (int)(w1 >> 20); }
+    __device__ __forceinline__ int ccb() const { return (int)(w2 << 16) >> 16; }
+    __device__ __forceinline__ int clk() const { return (int)(w2 >> 16); }
+    __device__ __forceinline__ int bid() const { return (int)(w3 & 0xffffu); }
+    __device__ __forceinline__ int bcm() const { return (int)(w3 >> 16); }
 };
 template <bool RZ>
 __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16Geo &g, int kb, const Smem16 &S,
@@ -270,18 +338,15 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
     const int zb = tz * kb + (RZ ? kb - 1 - p.zbs : p.zbs);   // kb: compile-time in the fixed instance
     const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < g.nzb;
     b.seg = valid ? col + zoff16(zb) : OOB;
+    b.lseg = pos_valid(p, nstream) && (meta & C_BLK) && (zb & ~1) < g.nzb ? col + zoff16(zb) : OOB;
     const int zu = RZ ? zb * 16 + 16 : zb * 16 - 1;          // z-upwind node of the brick's first slot
     b.zh = (valid && (meta & C_ZH) && p.zbs == 0) ? col + zoff16(zu >> 4) + (uint32_t)(zu & 15) * 4u : OOB;
-    b.zb = valid ? zb : 0;
-    b.ri = p.ri;
-    b.clk = p.sp;
-    b.bid = S.ring_b[p.ri];
     int fl = valid ? (int)((meta & 0x7f) | F_VALID) : 0;
     if (zb == (RZ ? g.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : g.nzb - 1)) fl |= F_LAST;
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
     bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && zb * 16 + 16 > L.nz);
-    b.bcm = 0;
+    unsigned bcm = 0;
     if (__any(fl & C_BC)) {
         // BC z-slots of this column segment (rare: columns through a source box)
         const int e = S.ring_e[p.ri];
@@ -297,12 +362,14 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
                 }
             }
         }
-        b.bcm = (int)m;
+        bcm = m;
         slow |= m != 0;
     }
     if (slow) fl |= F_SLOW;
-    b.fl = fl;
-    b.ccb = ci_ccb(meta) + zb * 4;                             // nrz = 4: cell of node z = base + z / 4
+    const int ccb = ci_ccb(meta) + zb * 4;                     // nrz = 4: cell of node z = base + z / 4
+    b.w1 = (uint32_t)fl | ((uint32_t)(valid ? zb : 0) << 12) | ((uint32_t)p.ri << 20);
+    b.w2 = ((uint32_t)ccb & 0xffffu) | ((uint32_t)p.sp << 16);
+    b.w3 = ((uint32_t)S.ring_b[p.ri] & 0xffffu) | (bcm << 16);
     return b;
 }
 // this lane's half (8 z) of halo column j at the edge lane's position pe
@@ -486,10 +553,10 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
 {
     const int lane = threadIdx.x;
     const float T = (float)L.conv_thresh;
-    const int fl = b0.fl;
+    const int fl = b0.fl();
     bool xp = true, xn = true, yp = true, yn = true, act = true;
     if (GENERIC) {
-        const int e = S.ring_e[b0.ri];
+        const int e = S.ring_e[b0.ri()];
         const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
         const bool xlo = x > 0, xhi = x < L.nx - 1, ylo = y > 0, yhi = y < L.ny - 1;
         xp = rx ? xhi : xlo; xn = rx ? xlo : xhi; yp = ry ? yhi : ylo; yn = ry ? ylo : yhi;
@@ -501,25 +568,34 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
     const int rxp = lxs < 7 ? lane + 1 : 64 + lys, ryp = lys < 7 ? lane + 8 : 72 + lxs;
     float fc = 0.f, ffc = 0.f, ff2c = 0.f, ff3c = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < 2; hh++) {
-        // the half of the brick this pass updates (sweep order: low z first
-        // unless RZ) and the four neighbour rows' values for it
-        const int h = RZ ? 1 - hh : hh;
-        float xm[8], xq[8], ym[8], yq[8];
-        load_half16(S.xr, 0, rxm, h, xm);
-        load_half16(S.xr, 0, rym, h, ym);
-        load_half16(S.xr, 1, rxp, h, xq);
-        load_half16(S.xr, 1, ryp, h, yq);
+    for (int hh = 0; hh < MCEIK16_NPASS; hh++) {
+        // the part of the brick this pass updates (sweep order: low z first
+        // unless RZ) and the four neighbour rows' values for it: halves (8 z,
+        // MCEIK16_NPASS 2) or quarters (4 z, 4: half the neighbour registers)
+        constexpr int PZ = 16 / MCEIK16_NPASS;
+        const int h = RZ ? MCEIK16_NPASS - 1 - hh : hh;
+        float xm[PZ], xq[PZ], ym[PZ], yq[PZ];
+        if (PZ == 8) {
+            load_half16(S.xr, 0, rxm, h, *reinterpret_cast<float (*)[8]>(&xm[0]));
+            load_half16(S.xr, 0, rym, h, *reinterpret_cast<float (*)[8]>(&ym[0]));
+            load_half16(S.xr, 1, rxp, h, *reinterpret_cast<float (*)[8]>(&xq[0]));
+            load_half16(S.xr, 1, ryp, h, *reinterpret_cast<float (*)[8]>(&yq[0]));
+        } else {
+            lds_r4(S.xr + XROW16(0, h, rxm), xm[0], xm[1], xm[2], xm[3]);
+            lds_r4(S.xr + XROW16(0, h, rym), ym[0], ym[1], ym[2], ym[3]);
+            lds_r4(S.xr + XROW16(1, h, rxp), xq[0], xq[1], xq[2], xq[3]);
+            lds_r4(S.xr + XROW16(1, h, ryp), yq[0], yq[1], yq[2], yq[3]);
+        }
 #pragma unroll
-        for (int jj = 0; jj < 8; jj++) {
-            const int j = hh * 8 + jj;                      // sweep-order slot
+        for (int jj = 0; jj < PZ; jj++) {
+            const int j = hh * PZ + jj;                     // sweep-order slot
             const int pj = RZ ? 15 - j : j;                 // z slot
-            const int ph = pj & 7;                          // index in the half
+            const int ph = pj % PZ;                         // index in the pass
             const int pprev = RZ ? pj + 1 : pj - 1, pnext = RZ ? pj - 1 : pj + 1;
             const float self = v[pj];
             if (!GENERIC) {
-                if (jj == 0 || jj == 4) {                   // a new cell (4 z per cell) in sweep order
-                    fc = S.cc[b0.ccb + (pj >> 2)];
+                if ((j & 3) == 0) {                        // a new cell (4 z per cell) in sweep order
+                    fc = S.cc[b0.ccb() + (pj >> 2)];
                     ffc = fc * fc;
                     ff2c = ffc + ffc;
                     ff3c = 3.0f * ffc;
@@ -529,7 +605,7 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
             float zup, zdn;
             if (GENERIC) {
                 xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
-                const int zabs = b0.zb * 16 + pj;
+                const int zabs = b0.zb() * 16 + pj;
                 const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
                 const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
                 zup = zp_ex ? (j > 0 ? v[pprev] : zprev0) : self;
@@ -541,12 +617,12 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
             const float ux = fmin_(xup, xdn), uy = fmin_(yup, ydn), uz = fmin_(zup, zdn);
             float nv;
             if (GENERIC) {
-                const int zabs = b0.zb * 16 + pj;
+                const int zabs = b0.zb() * 16 + pj;
                 const int zc_ = zabs < L.nz ? zabs : L.nz - 1;          // cut brick: clamp the cell
-                const float f = S.cc[b0.ccb - b0.zb * 4 + (zc_ >> 2)];
+                const float f = S.cc[b0.ccb() - b0.zb() * 4 + (zc_ >> 2)];
                 int e;
                 const float ub = godunov_bl<true>(ux, uy, uz, f, e);
-                const bool upd = act && zabs < L.nz && !((b0.bcm >> pj) & 1);
+                const bool upd = act && zabs < L.nz && !((b0.bcm() >> pj) & 1);
                 nv = upd ? fmin_(self, ub) : self;
                 if ((fl & C_00) && zabs == 0) ierr_last = upd ? e : 0;
             } else {
@@ -587,7 +663,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
 
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
+    constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
     float v[16], qa[16], hq[8], hn[8];
+    LineLd lq;                                       // FL: this step's line loads
+    float hp[8];                                     // FL: the half held from the previous step
     float zc, zn, zq;
     float ccv[CCR];
     int ccsize = 0;
@@ -654,6 +733,27 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             seg_finish(t, n);
             store_row16(S.xr, 1, lane, n);
         }
+    }
+    if (FL) {
+        // the held half for step 0: the lane whose step-0 target is the second
+        // brick of its position (it would have loaded the line one step
+        // earlier) gets it from its own segment, quarters split over the pair
+        Pos pn = p3;
+        pos_adv(pn, kb, nr);
+        const bool nl = pn.vb >= 0 && pn.zbs == 1;
+        const uint32_t sn = nl ? brick_info16<RZ>(L, g, kb, S, pn, nstream, lx, ly, bc, S.meta[pn.ri * 64 + lane],
+                                                  S.ring_base[pn.ri] + lanecol).seg
+                               : OOB;
+        const bool nlp = dpp_swap_pair((unsigned)nl) != 0u;
+        const uint32_t snp = dpp_swap_pair(sn);
+        const uint32_t s0 = (nl ? sn : (nlp ? snp : OOB)) + (uint32_t)(lane & 1) * 16u;
+        float t[4];
+        bload4(ur, s0, t);
+        hp[0] = t[0]; hp[1] = t[1]; hp[2] = t[2]; hp[3] = t[3];
+        bload4(ur, s0 + 32u, t);
+        hp[4] = t[0]; hp[5] = t[1]; hp[6] = t[2]; hp[7] = t[3];
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hp[i]));
     }
     pos_adv(pe, kb, nr);
     {
@@ -723,7 +823,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         const uint32_t c3 = S.ring_base[p3.ri] + lanecol, ce = S.ring_base[pe.ri] + hcol;
         __builtin_amdgcn_sched_barrier(0);
         const BInfo16 b3 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, m3, c3);
-        seg_issue(ur, b3.seg, qa);
+        if (FL)
+            line_issue(ur, b3.lseg, p3.vb >= 0 && p3.zbs == 0, lq);
+        else
+            seg_issue(ur, b3.seg, qa);
         zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
         {
             const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
@@ -734,24 +837,40 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             TRAF(S, 2, b3.zh != OOB, 4);
         }
         // ---- u0: old values of a block's first visit in the iteration (< T only)
-        if (__any(b0.fl & C_U0)) {
+        if (__any(b0.fl() & C_U0)) {
             unsigned m = __builtin_bit_cast(unsigned, v[0]);
 #pragma unroll
             for (int i = 1; i < 16; i++) m = min(m, __builtin_bit_cast(unsigned, v[i]));
-            const bool st0 = __builtin_bit_cast(float, m) < (float)L.conv_thresh && (b0.fl & C_U0);
+            const bool st0 = __builtin_bit_cast(float, m) < (float)L.conv_thresh && (b0.fl() & C_U0);
             if (__any(st0)) store16_plain(u0r, st0 ? b0.seg : OOB, v);
             TRAF(S, 4, st0, 64);
         }
         // ---- the 16 z-slots of the current brick (next brick's first value
         // in sweep order from this lane's XN row)
         const float znext = S.xr[XROW16(1, RZ ? 3 : 0, lane) + (RZ ? 3 : 0)];
-        const float zp0 = (b0.fl & F_ZH) ? zc : zprev;
+        const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
         bool changed = false, nc = false;
-        if (__any(b0.fl & F_SLOW))
+        if (__any(b0.fl() & F_SLOW))
             brick16<RZ, true>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
         else
             brick16<RZ, false>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
-        const bool val = (b0.fl & F_VALID) != 0;
+#ifdef MCEIK_EXP_VALU
+        {   // sensitivity experiment: N extra dependent VALU per step (results unchanged)
+            unsigned x = (unsigned)B;
+#pragma unroll
+            for (int k = 0; k < MCEIK_EXP_VALU; k++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x));
+            asm volatile("" ::"v"(x));
+        }
+#endif
+#ifdef MCEIK_EXP_LOAD
+        if ((B & (MCEIK_EXP_LOAD - 1)) == 0) {   // sensitivity experiment: extra 64 B/lane from the u0 scratch
+            float t[4], w[4];
+            bload4(u0r, b0.seg, t);
+            bload4(u0r, b0.seg == OOB ? OOB : b0.seg + 32u, w);
+            asm volatile("" ::"v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+        }
+#endif
+        const bool val = (b0.fl() & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
         nchg += changed ? 2u : 0u;                   // in 8-z segment equivalents
@@ -760,7 +879,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         if (cc_pend >= 0) cc_write<float, CCR>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
         cc_pend = ccfill ? ccri : -1;
         float nn[16];
-        if (MCEIK16_PAIR) {
+        if (FL) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) asm volatile("" : "+v"(lq.a[i]), "+v"(lq.h[i]));
+        } else if (MCEIK16_PAIR) {
 #pragma unroll
             for (int i = 0; i < 16; i++) nn[i] = qa[i];     // raw quarters (raw_write below)
         } else {
@@ -770,8 +892,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
 #pragma unroll
         for (int i = 0; i < 8; i++) hq[i] = hn[i];
         zc = zn; zn = zq;
+        if (!FL) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) asm volatile("" : "+v"(nn[i]));
+            for (int i = 0; i < 16; i++) asm volatile("" : "+v"(nn[i]));
+        }
         asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]), "+v"(hq[4]), "+v"(hq[5]),
                      "+v"(hq[6]), "+v"(hq[7]));
         asm volatile("" : "+v"(zn));
@@ -790,12 +914,17 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             }
         }
         TRAF(S, 3, changed, 64);
-        if (changed) S.lastchg[b0.bid] = (unsigned short)(clock0 + b0.clk);
+        if (changed) S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
         load_row16(S.xr, 1, lane, v);
-        if (MCEIK16_PAIR)
+        if (FL) {
+            line_write(S.xr, lq, hp);
+#pragma unroll
+            for (int i = 0; i < 8; i++) hp[i] = lq.h[i];
+        } else if (MCEIK16_PAIR) {
             raw_write(S.xr, pbn, nn);
-        else
+        } else {
             store_row16(S.xr, 1, lane, nn);
+        }
         asm volatile("" ::: "memory");
         b0 = b1;
         b1 = b3;

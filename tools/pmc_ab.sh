@@ -14,8 +14,8 @@ for v in ${AB_VARIANTS}; do
   i=0
   for P in "${GROUPS_[@]}"; do
     i=$((i+1))
-    timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex fsm_solve_kernel -d "$OUT/$v/pass$i" -o pmc \
-        --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/$v/bench_pass$i.log" 2>&1
+    timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex "fsm16_solve_kernel|fsm_solve_kernel" -d "$OUT/$v/pass$i" -o pmc \
+        --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --pipes 1 > "$OUT/$v/bench_pass$i.log" 2>&1
   done
 done
 cp /tmp/lib_keep.so mceik_amd/libmceik_hip.so
