@@ -119,6 +119,9 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 #ifndef MCEIK16_FULLLINE
 #define MCEIK16_FULLLINE 1       // the fixed instance (2-step positions) loads whole own lines
 #endif
+#ifndef MCEIK16_LEAN
+#define MCEIK16_LEAN 1           // the fixed instance decodes lean position words
+#endif
 #ifndef MCEIK16_NPASS
 #define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
 #endif
@@ -321,7 +324,7 @@ struct BInfo16 {
                              // (prefetch only: a line loader whose own brick is past the grid end)
     uint32_t w1, w2, w3;
     __device__ __forceinline__ int fl() const { return (int)(w1 & 0xfffu); }
-    __device__ __forceinline__ int zb() const { return (int)((w1 >> 12) & 0xffu); }
+    __device__ __forceinline__ int zb() const { return (int)((w1 >> 12) & 0xffu); }   // (lean: the phase)
     __device__ __forceinline__ int ri() const { return (int)(w1 >> 20); }
     __device__ __forceinline__ int ccb() const { return (int)(w2 << 16) >> 16; }
     __device__ __forceinline__ int clk() const { return (int)(w2 >> 16); }
@@ -381,6 +384,101 @@ __device__ __forceinline__ uint32_t halo_offset16(const Fsm16Geo &g, int kb, con
     const bool valid = pos_valid(pe, nstream) && (meta & C_BLK) && zb < g.nzb;
     const uint32_t base = col + ((meta & hbit) ? 0u : hdelta);
     return valid ? base + zoff16(zb) + (uint32_t)half * 32u : OOB;
+}
+
+// ---- lean position words (the fixed instance: 2-step positions) ---------
+// At admission every lane's position word holds its column flags (bits 0-8,
+// as column_word's), per sweep-order phase p a group g_p = FIRST | LAST << 1
+// | SLOW << 2 | ZH << 3 | VALID << 4 at bits 9 + 5p, and the cell-cache base
+// of the phase-0 brick at bits 19-31; ring_base holds the position's line
+// base (tile offset + tz << 13).  A step then decodes its brick with a few
+// shifts instead of rederiving zb, validity and the brick flags from tz.
+#define LW_G(p) (9 + 5 * (p))
+#define LW_CCB 19
+template <bool RZ>
+__device__ __forceinline__ unsigned lean_word(const FsmLaunch &L, const Fsm16Geo &g, const ColTile &ct, int tz, int ri,
+                                              int u0flag, int zh)
+{
+    int cz0, nczb;
+    block_zcells(L, L.kb, tz, cz0, nczb);
+    const int m = ct.fl | C_BLK | (u0flag ? C_U0 : 0) | (zh ? C_ZH : 0);
+    const int zb0 = 2 * tz + (RZ ? 1 : 0);                      // the phase-0 brick (sweep order)
+    unsigned w = (unsigned)m & 0x1ffu;
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+        const int zb = RZ ? zb0 - p : zb0 + p;
+        unsigned gp = zb < g.nzb ? 16u : 0u;
+        if (zb == (RZ ? g.nzb - 1 : 0)) gp |= 1u;
+        if (zb == (RZ ? 0 : g.nzb - 1)) gp |= 2u;
+        if ((m & C_PART) || ((m & C_00) && zb == 0) || zb * 16 + 16 > L.nz) gp |= 4u;
+        if (p == 0 && (m & C_ZH)) gp |= 8u;
+        w |= gp << LW_G(p);
+    }
+    const int ccb0 = ri * L.ccb + ct.cl * nczb - cz0 + zb0 * 4;
+    return w | ((unsigned)ccb0 << LW_CCB);
+}
+template <bool RZ>
+__device__ __forceinline__ BInfo16 brick_info_lean(const FsmLaunch &L, const Smem16 &S, const Pos &p, int nstream,
+                                                   int lx, int ly, const BcBoxes &bc, unsigned w, uint32_t base)
+{
+    BInfo16 b;
+    const int ph = p.zbs;
+    const unsigned gp = (w >> (ph ? LW_G(1) : LW_G(0))) & 31u;
+    const bool pv = pos_valid(p, nstream);
+    const bool valid = pv && (gp & 16u);
+    const uint32_t off = base + ((uint32_t)(ph ^ (RZ ? 1 : 0)) << 6);
+    b.seg = valid ? off : OOB;
+    b.lseg = pv && (w & ((16u << LW_G(0)) | (16u << LW_G(1)))) ? off : OOB;
+    b.zh = valid && (gp & 8u) ? off + (RZ ? 8192u - 64u : 124u - 8192u) : OOB;
+    int fl = valid ? (int)((w & 0x7fu) | F_VALID | ((gp & 15u) << 8)) : 0;
+    unsigned bcm = 0;
+    if (__any(fl & C_BC)) {
+        // BC z-slots of this column segment (rare: columns through a source box)
+        const int e = S.ring_e[p.ri];
+        const int zb = 2 * ((e >> 24) & 0xff) + (RZ ? 1 - ph : ph);
+        const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
+        if (fl & C_BC) {
+            for (int k = 0; k < bc.n; k++) {
+                const int *q = bc.box + 6 * k;
+                if (x >= q[0] && x <= q[1] && y >= q[2] && y <= q[3]) {
+                    int lo = q[4] - zb * 16, hi = q[5] - zb * 16;
+                    lo = lo < 0 ? 0 : lo; hi = hi > 15 ? 15 : hi;
+                    if (lo <= hi) bcm |= ((2u << hi) - (1u << lo));
+                }
+            }
+        }
+        if (bcm) fl |= F_SLOW;
+    }
+    const int ccb = (int)(w >> LW_CCB) + (RZ ? -4 * ph : 4 * ph);
+    b.w1 = (uint32_t)fl | ((uint32_t)ph << 12) | ((uint32_t)p.ri << 20);
+    b.w2 = ((uint32_t)ccb & 0xffffu) | ((uint32_t)p.sp << 16);
+    b.w3 = ((uint32_t)S.ring_b[p.ri] & 0xffffu) | (bcm << 16);
+    return b;
+}
+template <bool RZ>
+__device__ __forceinline__ uint32_t halo_offset_lean(const Pos &pe, int nstream, int half, unsigned me, uint32_t base,
+                                                     unsigned hbit, uint32_t hdelta)
+{
+    const int ph = pe.zbs;
+    const bool valid = pos_valid(pe, nstream) && ((me >> (ph ? LW_G(1) : LW_G(0))) & 16u);
+    const uint32_t o = base + ((me & hbit) ? 0u : hdelta) + ((uint32_t)(ph ^ (RZ ? 1 : 0)) << 6) + (uint32_t)half * 32u;
+    return valid ? o : OOB;
+}
+// the brick info / halo offset of a step: lean (fixed instance) or general
+template <bool RZ, bool LEAN>
+__device__ __forceinline__ BInfo16 brick_info_any(const FsmLaunch &L, const Fsm16Geo &g, int kb, const Smem16 &S,
+                                                  const Pos &p, int nstream, int lx, int ly, const BcBoxes &bc,
+                                                  unsigned meta, uint32_t col)
+{
+    if (LEAN) return brick_info_lean<RZ>(L, S, p, nstream, lx, ly, bc, meta, col);
+    return brick_info16<RZ>(L, g, kb, S, p, nstream, lx, ly, bc, meta, col);
+}
+template <bool RZ, bool LEAN>
+__device__ __forceinline__ uint32_t halo_offset_any(const Fsm16Geo &g, int kb, const Pos &pe, int nstream, int half,
+                                                    unsigned meta, uint32_t col, unsigned hbit, uint32_t hdelta)
+{
+    if (LEAN) return halo_offset_lean<RZ>(pe, nstream, half, meta, col, hbit, hdelta);
+    return halo_offset16<RZ>(g, kb, pe, nstream, half, meta, col, hbit, hdelta);
 }
 
 // Diagonal order of the tiles for the (+x, +y) sweep (build_order in
@@ -475,8 +573,10 @@ __device__ __forceinline__ int decide16(const FsmLaunch &L, const Fsm16Geo &g, c
 // column meta, lane 0 the ring entry, block id, tile base and the block's
 // visit clock.  u0 flag: the block's first visit in this iteration
 // (lastproc is rebased to 1 at every iteration start, iter_norm()).
-__device__ __forceinline__ void admit16(const FsmLaunch &L, const Smem16 &S, const BcBoxes &bc, int entry, int zh,
-                                        int ri, int C, int lx, int ly, int lxs, int lys, int rx, int ry, ColTile &ct)
+template <bool RZ, bool LEAN>
+__device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, const BcBoxes &bc,
+                                        int entry, int zh, int ri, int C, int lx, int ly, int lxs, int lys, int rx,
+                                        int ry, ColTile &ct)
 {
     unsigned meta = 0;
     int bid = 0, nbv = 0;
@@ -487,8 +587,8 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Smem16 &S, con
         nbv = min(L.kb, L.nzb - tz * L.kb);          // 8-z bricks of the block (visit statistics)
         const int u0flag = S.lastproc[bid] < 64;       // no visit since the iteration started (clock 64)
         if ((entry & 0xffffff) != ct.tile) column_tile<float>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
-        meta = column_word(L, L.kb, ct, tz, ri, u0flag, zh);
-        base = (uint32_t)(ty * L.ntx + tx) * tile_bytes<float>(L);
+        meta = LEAN ? lean_word<RZ>(L, g, ct, tz, ri, u0flag, zh) : column_word(L, L.kb, ct, tz, ri, u0flag, zh);
+        base = (uint32_t)(ty * L.ntx + tx) * tile_bytes<float>(L) + (LEAN ? (uint32_t)tz << 13 : 0u);
     }
     const int nact = L.visit_stats && entry >= 0 ? __builtin_popcountll(__ballot(ct.fl & C_ACT)) : 0;
     asm volatile("" ::: "memory");
@@ -546,7 +646,7 @@ __device__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
 // fsm_kernel.hip brick_update (grid-edge columns of cut tiles, cut z-bricks,
 // BC nodes, node (0,0,0)); otherwise every lane's missing x/y neighbours are
 // already its own old values (the halo of a grid-edge lane is its column).
-template <bool RZ, bool GENERIC>
+template <bool RZ, bool GENERIC, bool LEAN>
 __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, const BInfo16 &b0, float (&v)[16],
                                         float zprev0, float znext, int lx, int ly, int rx, int ry, bool &changed,
                                         bool &nc, int &ierr_last)
@@ -555,8 +655,10 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
     const float T = (float)L.conv_thresh;
     const int fl = b0.fl();
     bool xp = true, xn = true, yp = true, yn = true, act = true;
+    int zbg = 0;                                             // the brick's zb (generic path)
     if (GENERIC) {
         const int e = S.ring_e[b0.ri()];
+        zbg = LEAN ? 2 * ((e >> 24) & 0xff) + (RZ ? 1 - b0.zb() : b0.zb()) : b0.zb();
         const int x = (e & 0xfff) * 8 + lx, y = ((e >> 12) & 0xfff) * 8 + ly;
         const bool xlo = x > 0, xhi = x < L.nx - 1, ylo = y > 0, yhi = y < L.ny - 1;
         xp = rx ? xhi : xlo; xn = rx ? xlo : xhi; yp = ry ? yhi : ylo; yn = ry ? ylo : yhi;
@@ -605,7 +707,7 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
             float zup, zdn;
             if (GENERIC) {
                 xup = xp ? xup : self; xdn = xn ? xdn : self; yup = yp ? yup : self; ydn = yn ? ydn : self;
-                const int zabs = b0.zb() * 16 + pj;
+                const int zabs = zbg * 16 + pj;
                 const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
                 const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
                 zup = zp_ex ? (j > 0 ? v[pprev] : zprev0) : self;
@@ -617,9 +719,9 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
             const float ux = fmin_(xup, xdn), uy = fmin_(yup, ydn), uz = fmin_(zup, zdn);
             float nv;
             if (GENERIC) {
-                const int zabs = b0.zb() * 16 + pj;
+                const int zabs = zbg * 16 + pj;
                 const int zc_ = zabs < L.nz ? zabs : L.nz - 1;          // cut brick: clamp the cell
-                const float f = S.cc[b0.ccb() - b0.zb() * 4 + (zc_ >> 2)];
+                const float f = S.cc[b0.ccb() - zbg * 4 + (zc_ >> 2)];
                 int e;
                 const float ub = godunov_bl<true>(ux, uy, uz, f, e);
                 const bool upd = act && zabs < L.nz && !((b0.bcm() >> pj) & 1);
@@ -664,6 +766,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
+    constexpr bool LEAN = KB16 == 2 && MCEIK16_LEAN;     // lean position words (2-step positions)
     float v[16], qa[16], hq[8], hn[8];
     LineLd lq;                                       // FL: this step's line loads
     float hp[8];                                     // FL: the half held from the previous step
@@ -683,7 +786,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             nstream = pos;
             break;
         }
-        admit16(L, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
+        admit16<RZ, LEAN>(L, g, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
         if (e >= 0) {
             cc_issue<CCR>(L, L.kb, sr, e, ccv, ccsize);
             TRAFU(S, 5, ccsize * 4);
@@ -696,7 +799,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     // bricks vb (b0) and vb+1 (b1); the loop computes vb+2's (b3) and carries it
     Pos p3, pe;
     pos_init(p3, -d, kb, nr);
-    BInfo16 b0 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
+    BInfo16 b0 = brick_info_any<RZ, LEAN>(L, g, kb, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
                                   S.ring_base[p3.ri] + lanecol);
     const int pbr = pair_row(0, lane), pbn = pair_row(1, lane);
     {
@@ -711,7 +814,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     }
     pos_init(pe, -hd, kb, nr);
     {
-        const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
+        const uint32_t ho = halo_offset_any<RZ, LEAN>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
         bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hq[0]));
         bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hq[4]));
@@ -721,7 +824,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     TRAF(S, 0, b0.seg != OOB, 64);
     TRAF(S, 2, b0.zh != OOB, 4);
     pos_adv(p3, kb, nr);
-    BInfo16 b1 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
+    BInfo16 b1 = brick_info_any<RZ, LEAN>(L, g, kb, S, p3, nstream, lx, ly, bc, S.meta[p3.ri * 64 + lane],
                                   S.ring_base[p3.ri] + lanecol);
     {
         float t[16];
@@ -741,7 +844,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         Pos pn = p3;
         pos_adv(pn, kb, nr);
         const bool nl = pn.vb >= 0 && pn.zbs == 1;
-        const uint32_t sn = nl ? brick_info16<RZ>(L, g, kb, S, pn, nstream, lx, ly, bc, S.meta[pn.ri * 64 + lane],
+        const uint32_t sn = nl ? brick_info_any<RZ, LEAN>(L, g, kb, S, pn, nstream, lx, ly, bc, S.meta[pn.ri * 64 + lane],
                                                   S.ring_base[pn.ri] + lanecol).seg
                                : OOB;
         const bool nlp = dpp_swap_pair((unsigned)nl) != 0u;
@@ -757,7 +860,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     }
     pos_adv(pe, kb, nr);
     {
-        const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
+        const uint32_t ho = halo_offset_any<RZ, LEAN>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
         bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
         bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
@@ -799,7 +902,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             if (e == -2) {
                 nstream = pos;
             } else {
-                admit16(L, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
+                admit16<RZ, LEAN>(L, g, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
                 if (e >= 0) {
                     cc_issue<CCR>(L, L.kb, sr, e, ccv, ccsize);
                     TRAFU(S, 5, ccsize * 4);
@@ -822,14 +925,14 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         const unsigned m3 = S.meta[p3.ri * 64 + lane], me = S.meta[pe.ri * 64 + he];
         const uint32_t c3 = S.ring_base[p3.ri] + lanecol, ce = S.ring_base[pe.ri] + hcol;
         __builtin_amdgcn_sched_barrier(0);
-        const BInfo16 b3 = brick_info16<RZ>(L, g, kb, S, p3, nstream, lx, ly, bc, m3, c3);
+        const BInfo16 b3 = brick_info_any<RZ, LEAN>(L, g, kb, S, p3, nstream, lx, ly, bc, m3, c3);
         if (FL)
             line_issue(ur, b3.lseg, p3.vb >= 0 && p3.zbs == 0, lq);
         else
             seg_issue(ur, b3.seg, qa);
         zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
         {
-            const uint32_t ho = halo_offset16<RZ>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
+            const uint32_t ho = halo_offset_any<RZ, LEAN>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
             bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
             bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
             TRAF(S, 1, ho != OOB, 32);
@@ -851,9 +954,9 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
         bool changed = false, nc = false;
         if (__any(b0.fl() & F_SLOW))
-            brick16<RZ, true>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
+            brick16<RZ, true, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
         else
-            brick16<RZ, false>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
+            brick16<RZ, false, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
 #ifdef MCEIK_EXP_VALU
         {   // sensitivity experiment: N extra dependent VALU per step (results unchanged)
             unsigned x = (unsigned)B;
