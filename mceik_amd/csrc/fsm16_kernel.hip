@@ -208,6 +208,11 @@ __device__ __forceinline__ void raw_read(const float *x, int pb, float (&a)[16])
     lds_r4(x + pb + 4, a[8], a[9], a[10], a[11]);
     lds_r4(x + pb + 2 * XQE + 4, a[12], a[13], a[14], a[15]);
 }
+template <int P>
+struct Par16 {
+    static constexpr int value = P;
+};
+
 // ---- full-line own loads (FL: positions of 2 steps = one 128-B line per column)
 // A lane's position covers its column's whole 128-B line (two 16-z bricks);
 // x-adjacent lanes (a pair) run one step apart, so at every step exactly one
@@ -223,10 +228,10 @@ __device__ __forceinline__ void raw_read(const float *x, int pb, float (&a)[16])
 // which the L2 re-fetched between the halves.
 struct LineLd {
     float a[8];                  // now half: quarters p, p+2 of the loader's line
-    float h[8];                  // later half: quarters p, p+2 (held one step)
     int rowl, rowo;              // XN rows: the loader's, the other lane's
 };
-__device__ __forceinline__ void line_issue(Rsrc r, uint32_t seg, bool isl, LineLd &q)
+// the later half (quarters p, p+2) goes to h, held one step
+__device__ __forceinline__ void line_issue(Rsrc r, uint32_t seg, bool isl, LineLd &q, float (&h)[8])
 {
     const int lane = threadIdx.x, par = lane & 1;
     const bool islp = dpp_swap_pair((unsigned)isl) != 0u;
@@ -240,9 +245,9 @@ __device__ __forceinline__ void line_issue(Rsrc r, uint32_t seg, bool isl, LineL
     q.a[4] = t[0]; q.a[5] = t[1]; q.a[6] = t[2]; q.a[7] = t[3];
     const uint32_t sh = sl ^ 64u;                               // the other half of the line (OOB stays OOB)
     bload4(r, sh + o, t);
-    q.h[0] = t[0]; q.h[1] = t[1]; q.h[2] = t[2]; q.h[3] = t[3];
+    h[0] = t[0]; h[1] = t[1]; h[2] = t[2]; h[3] = t[3];
     bload4(r, sh + o + 32u, t);
-    q.h[4] = t[0]; q.h[5] = t[1]; q.h[6] = t[2]; q.h[7] = t[3];
+    h[4] = t[0]; h[5] = t[1]; h[6] = t[2]; h[7] = t[3];
     q.rowl = isl ? lane : (lane ^ 1);
     q.rowo = lane ^ (q.rowl == lane ? 1 : 0);
 }
@@ -767,9 +772,16 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
     constexpr bool LEAN = KB16 == 2 && MCEIK16_LEAN;     // lean position words (2-step positions)
-    float v[16], qa[16], hq[8], hn[8];
+    // ping-pong register sets by step parity (the step loop runs in pairs, so
+    // no register copies at the loop latch): halo values hs[p] loaded at the
+    // step before, staged at the end of step p, hs[1 - p] loading; FL's held
+    // line half hps[p] from the step before, hps[1 - p] loading
+    float v[16], qa[16], hs[2][8];
     LineLd lq;                                       // FL: this step's line loads
-    float hp[8];                                     // FL: the half held from the previous step
+    float hps[2][8];                                 // FL: held line halves
+    float (&hq)[8] = hs[0];                          // prologue names: halo of step 0, of step 1
+    float (&hn)[8] = hs[1];
+    float (&hp)[8] = hps[0];
     float zc, zn, zq;
     float ccv[CCR];
     int ccsize = 0;
@@ -877,13 +889,14 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     }
     halo_stage16(S.xr, lane, hq);
     float zprev = UN;                                // last slot of the previous brick (sweep order)
+    // the prologue's loads are waited for here, once per sweep; step 0 stages
+    // hs[0] = the halos loaded second (hn)
 #pragma unroll
-    for (int i = 0; i < 8; i++) hq[i] = hn[i];
-    // the prologue's loads are waited for here, once per sweep
+    for (int i = 0; i < 8; i++) hs[0][i] = hs[1][i];
 #pragma unroll
     for (int i = 0; i < 16; i++) asm volatile("" : "+v"(v[i]));
 #pragma unroll
-    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hq[i]));
+    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hs[0][i]));
     asm volatile("" : "+v"(zc), "+v"(zn));
     asm volatile("" ::: "memory");
 
@@ -917,7 +930,12 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     auto more = [&]() __attribute__((always_inline)) -> bool {
         return !(nstream != 0x7fffffff && B >= nstream * kb + 14);
     };
-    auto step = [&]() __attribute__((always_inline)) -> bool {
+    auto step = [&](auto par) __attribute__((always_inline)) -> bool {
+        constexpr int P = FL ? decltype(par)::value : 0;   // other instances: one set + copies
+        float (&hcur)[8] = hs[P];                    // staged at the end of this step
+        float (&hnew)[8] = hs[1 - P];                // loaded this step
+        float (&hpcur)[8] = hps[P];                  // FL: written to XN at the end of this step
+        float (&hpnew)[8] = hps[1 - P];              // FL: loaded this step
         // ---- prefetch: own segment and halos of vb+2 (consumed at the end of
         // this step, before its stores; halos staged at the end of the next)
         pos_adv(p3, kb, nr);
@@ -927,14 +945,14 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         __builtin_amdgcn_sched_barrier(0);
         const BInfo16 b3 = brick_info_any<RZ, LEAN>(L, g, kb, S, p3, nstream, lx, ly, bc, m3, c3);
         if (FL)
-            line_issue(ur, b3.lseg, p3.vb >= 0 && p3.zbs == 0, lq);
+            line_issue(ur, b3.lseg, p3.vb >= 0 && p3.zbs == 0, lq, hpnew);
         else
             seg_issue(ur, b3.seg, qa);
         zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
         {
             const uint32_t ho = halo_offset_any<RZ, LEAN>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
-            bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
-            bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
+            bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hnew[0]));
+            bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hnew[4]));
             TRAF(S, 1, ho != OOB, 32);
             TRAF(S, 0, b3.seg != OOB, 64);
             TRAF(S, 2, b3.zh != OOB, 4);
@@ -984,23 +1002,25 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         float nn[16];
         if (FL) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) asm volatile("" : "+v"(lq.a[i]), "+v"(lq.h[i]));
+            for (int i = 0; i < 8; i++) asm volatile("" : "+v"(lq.a[i]), "+v"(hpnew[i]));
         } else if (MCEIK16_PAIR) {
 #pragma unroll
             for (int i = 0; i < 16; i++) nn[i] = qa[i];     // raw quarters (raw_write below)
         } else {
             seg_finish(qa, nn);
         }
-        halo_stage16(S.xr, lane, hq);
-#pragma unroll
-        for (int i = 0; i < 8; i++) hq[i] = hn[i];
+        halo_stage16(S.xr, lane, hcur);
         zc = zn; zn = zq;
         if (!FL) {
 #pragma unroll
             for (int i = 0; i < 16; i++) asm volatile("" : "+v"(nn[i]));
         }
-        asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]), "+v"(hq[4]), "+v"(hq[5]),
-                     "+v"(hq[6]), "+v"(hq[7]));
+        if (!FL) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) hcur[i] = hnew[i];
+        }
+        asm volatile("" : "+v"(hnew[0]), "+v"(hnew[1]), "+v"(hnew[2]), "+v"(hnew[3]), "+v"(hnew[4]), "+v"(hnew[5]),
+                     "+v"(hnew[6]), "+v"(hnew[7]));
         asm volatile("" : "+v"(zn));
         asm volatile("" ::: "memory");
         // ---- rows for the next step: results (XR), then this lane's next
@@ -1020,9 +1040,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         if (changed) S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
         load_row16(S.xr, 1, lane, v);
         if (FL) {
-            line_write(S.xr, lq, hp);
-#pragma unroll
-            for (int i = 0; i < 8; i++) hp[i] = lq.h[i];
+            line_write(S.xr, lq, hpcur);
         } else if (MCEIK16_PAIR) {
             raw_write(S.xr, pbn, nn);
         } else {
@@ -1038,8 +1056,14 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     };
     decide_step();
     if (more()) {
-        do {
-        } while (step());
+        if (FL) {
+            do {
+                if (!step(Par16<0>())) break;
+            } while (step(Par16<1>()));
+        } else {
+            do {
+            } while (step(Par16<0>()));
+        }
     }
     return nstream;
 }
