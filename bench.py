@@ -255,7 +255,7 @@ def main():
             gather_check = bool(torch.equal(tv.to(dev), post) and torch.equal(tl.to(dev), post_l))
         if comm is not None:
             comm.close()
-    fsm_ms, nlaunch, iters, (bricks, segs, segs_changed) = smp.fsm_stats()
+    fsm_ms, nlaunch, iters, (bricks, segs, segs_changed, wsteps) = smp.fsm_stats()
     _, logl, nacc, _ = smp.state()
     smp.close()
 
@@ -341,6 +341,7 @@ def main():
                          "iterations_per_solve": round(iters / steps / solves_per_step, 3),
                          "brick_visit_fraction": round(bricks / max(1.0, iters * 8.0 * nbricks), 4),
                          "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),
+                         "wave_steps_per_step": wsteps / steps,
                          "full_sweep_equiv_GBs": round(full_bytes / steps / step_fsm_s / 1e9, 1)},
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
@@ -355,7 +356,7 @@ def main():
                 line["gather"]["equals_torch_gather"] = gather_check
         if args.raw_stats:
             line["fsm_raw"] = {"bricks": bricks, "segs": segs, "segs_changed": segs_changed, "iters": iters,
-                               "launches": nlaunch}
+                               "wave_steps": wsteps, "launches": nlaunch}
         if cpu:
             line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         print(json.dumps(line), flush=True)

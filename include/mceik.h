@@ -132,9 +132,10 @@ int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *logl, const lo
                        long long step, int nkept);
 /* FSM accounting since init (or the last reset): kernel time of every FSM
  * launch from hipEvents on the sampler's stream (ms), launches, and the
- * sum over solves of executed iterations (8 sweeps each) and visits[3] = brick
+ * sum over solves of executed iterations (8 sweeps each) and visits[4] = brick
  * visits (8x8x8 nodes in one sweep; unchanged z-blocks are skipped), column
- * segments updated, segments changed (mceik_fsm_batch.visit_stats). Synchronises. */
+ * segments updated, segments changed, wave macro steps (mceik_fsm_batch.visit_stats).
+ * Synchronises. */
 int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsigned long long *iters,
                          unsigned long long *visits, int reset);
 int mceik_mcmc_finalize(mceik_mcmc **s);

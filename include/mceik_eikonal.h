@@ -131,9 +131,10 @@ typedef struct mceik_fsm_batch {
     unsigned long long *iter_total;  /* device counter += iterations of every solve, or NULL */
     int fast_sqrt;              /* 1: caller guarantees h*slowness >= 1e-12 (cells mode, fp32):
                                    use the shorter correctly rounded sqrt (same results) */
-    unsigned long long *visit_stats; /* device [3] += brick visits (8x8x8 nodes, one sweep; z-blocks
+    unsigned long long *visit_stats; /* device [4] += brick visits (8x8x8 nodes, one sweep; z-blocks
                                         whose inputs did not change are skipped), column segments
-                                        (8 nodes) updated, segments that changed; or NULL */
+                                        (8 nodes) updated, segments that changed, macro steps of the
+                                        sweep waves (one 64-lane step; 16 or 8 z per lane); or NULL */
     const int *solve_order;     /* device [nmodel*nstat]: work-queue slot -> solve id (a permutation;
                                    only the order solves start in changes), or NULL = model-major */
     unsigned long long *solve_clock; /* device [nmodel*nstat][2]: s_memrealtime (100 MHz) at the

@@ -1023,6 +1023,7 @@ extern "C" int mceik_relocate(const mceik_relocate_batch *b, void *stream)
 // MCMC sampler (include/mceik.h)
 #define MCEIK_EV_RING 32           // hipEvent pairs around timed FSM launches (fixed ring)
 #define MCEIK_MAX_PIPES 4
+#define MCEIK_ITERS_N (5 + MCEIK_TRAFFIC_N)   // d_iters: iterations, 4 visit statistics, traffic
 
 struct mceik_mcmc {
     McmcDev D;
@@ -1464,7 +1465,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     if (nphase > 1) rc |= dalloc(s, &D.ttab_cur, (size_t)nch * nphase * nstat * nev);
     rc |= dalloc(s, &d_niter, (size_t)nch * nphase * nstat);
     rc |= dalloc(s, &s->d_ierr, (size_t)nch * nphase * nstat);
-    rc |= dalloc(s, &s->d_iters, 4 + MCEIK_TRAFFIC_N);   // [0] iterations, [1..3] visit_stats, [4..] traffic
+    rc |= dalloc(s, &s->d_iters, MCEIK_ITERS_N);       // [0] iterations, [1..4] visit_stats, [5..] traffic
     if (s->max_samples) {
         rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncm);
         rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
@@ -1489,7 +1490,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
     b.visit_stats = s->d_iters + 1;
-    b.traffic = s->d_iters + 4;
+    b.traffic = s->d_iters + 5;
     b.max_waves = o->max_waves > 0 ? o->max_waves : 0;
     // f = h/v stays a normal float: the short correctly rounded sqrt (fp32 only)
     const int vhi = nphase == 2 ? std::max(o->vmax, o->vsmax) : o->vmax;
@@ -1553,7 +1554,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         mceik_mcmc_finalize(&s);
         return -1;
     }
-    hipMemset(s->d_iters, 0, (4 + MCEIK_TRAFFIC_N) * sizeof(unsigned long long));
+    hipMemset(s->d_iters, 0, MCEIK_ITERS_N * sizeof(unsigned long long));
     *out = s;
     return 0;
 }
@@ -1679,7 +1680,7 @@ extern "C" int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *log
         HIPCHK(hipMemcpy(D.logl, logl, (size_t)D.nchains * 8, hipMemcpyHostToDevice));
     } else {
         // one forward of the restored models (not timed, not counted in the FSM stats)
-        unsigned long long keep[4 + MCEIK_TRAFFIC_N];
+        unsigned long long keep[MCEIK_ITERS_N];
         HIPCHK(hipMemcpy(keep, s->d_iters, sizeof(keep), hipMemcpyDeviceToHost));
         if (mcmc_forward_all(s)) return -1;
         HIPCHK(mcmc_init_loglik(D, s->stream));
@@ -1791,28 +1792,28 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
         if (fold_launch(s, s->ev_folded)) return -1;
         s->ev_folded++;
     }
-    unsigned long long it[4 + MCEIK_TRAFFIC_N] = {0};
+    unsigned long long it[MCEIK_ITERS_N] = {0};
     HIPCHK(hipMemcpy(it, s->d_iters, sizeof(it), hipMemcpyDeviceToHost));
     {   // accounting build: requested bytes per launch by category
         unsigned long long tsum = 0;
-        for (int k = 0; k < MCEIK_TRAFFIC_N; k++) tsum += it[4 + k];
+        for (int k = 0; k < MCEIK_TRAFFIC_N; k++) tsum += it[5 + k];
         if (tsum && s->nlaunch) {
             static const char *nm[MCEIK_TRAFFIC_N] = {"own_load", "halo_load", "zup_load", "own_store",
                                                       "u0_store", "cell_load", "verify_load", "init_gather"};
             fprintf(stderr, "mceik traffic (requested bytes per FSM launch, %lld launches):", s->nlaunch);
-            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) fprintf(stderr, " %s=%.6e", nm[k], (double)it[4 + k] / s->nlaunch);
+            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) fprintf(stderr, " %s=%.6e", nm[k], (double)it[5 + k] / s->nlaunch);
             fprintf(stderr, " total=%.6e\n", (double)tsum / s->nlaunch);
         }
     }
     if (fsm_ms) *fsm_ms = s->fsm_ms;
     if (nlaunch) *nlaunch = s->nlaunch;
     if (iters) *iters = it[0];
-    if (visits) { visits[0] = it[1]; visits[1] = it[2]; visits[2] = it[3]; }
+    if (visits) { visits[0] = it[1]; visits[1] = it[2]; visits[2] = it[3]; visits[3] = it[4]; }
     if (reset) {
         s->fsm_ms = 0.0;
         s->nlaunch = 0;
         s->ev_folded = 0;
-        HIPCHK(hipMemset(s->d_iters, 0, (4 + MCEIK_TRAFFIC_N) * sizeof(unsigned long long)));
+        HIPCHK(hipMemset(s->d_iters, 0, MCEIK_ITERS_N * sizeof(unsigned long long)));
     }
     return 0;
 }

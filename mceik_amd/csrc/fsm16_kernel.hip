@@ -752,7 +752,7 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
 template <bool RZ, int KB16, int CCR>
 __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr,
                                        const BcBoxes &bc, const Smem16 &S, int rx, int ry, int clock0, bool &notconv,
-                                       int &ierr_last, unsigned &nchg)
+                                       int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
@@ -1065,6 +1065,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             } while (step(Par16<0>()));
         }
     }
+    nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     return nstream;
 }
 
@@ -1139,7 +1140,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         if (lane == 0)
             for (int k = 0; k < MCEIK_TRAFFIC_N; k++) S.scratch[8 + k] = 0;
 #endif
-        unsigned nchg = 0;
+        unsigned nchg = 0, nsteps = 0;
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<float, 1>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
@@ -1166,10 +1167,10 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
                         clock += g.infl + sweep16<true, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
-                                                              ierr_last, nchg);
+                                                              ierr_last, nchg, nsteps);
                     else
                         clock += g.infl + sweep16<false, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
-                                                               ierr_last, nchg);
+                                                               ierr_last, nchg, nsteps);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                     TRAF_FLUSH(L, S);
@@ -1192,6 +1193,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
                 atomicAdd(L.visit_stats, (unsigned long long)(unsigned)S.scratch[0]);
                 atomicAdd(L.visit_stats + 1, (unsigned long long)(unsigned)S.scratch[1]);
                 atomicAdd(L.visit_stats + 2, (unsigned long long)nchg);
+                atomicAdd(L.visit_stats + 3, (unsigned long long)nsteps);
             }
         }
         if (lane == 0) {

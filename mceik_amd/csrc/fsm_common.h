@@ -48,7 +48,7 @@ struct FsmLaunch {
     int fast_sqrt;               // host-validated: f = s*h is a normal float >= 1e-18
     unsigned *counter;           // 8 work-queue heads, 128 B apart (zeroed before the launch)
     unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
-    unsigned long long *visit_stats;  // [3] += tile visits, column-segment updates, changed segments; may be null
+    unsigned long long *visit_stats;  // [4] += brick visits, column-segment updates, changed segments, macro steps; may be null
     const int *solve_order;      // queue slot -> solve id, or null (slot = solve)
     unsigned long long *solve_clock;  // [nsolve][2] realtime at solve start / end, or null
     int max_waves;               // host only: cap on resident waves (0 = occupancy x CUs)

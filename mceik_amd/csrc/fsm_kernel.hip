@@ -528,7 +528,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
                                      const Smem<R> &S, int rx, int ry, int clock_it, int clock0,
-                                     bool &notconv, int &ierr_last, unsigned &nchg)
+                                     bool &notconv, int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
@@ -848,6 +848,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         while (step(c, n, hq, hn)) {
         }
     }
+    nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     return nstream;
 }
 
@@ -936,7 +937,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         if (lane == 0)
             for (int k = 0; k < MCEIK_TRAFFIC_N; k++) S.scratch[8 + k] = 0;
 #endif
-        unsigned nchg = 0;
+        unsigned nchg = 0, nsteps = 0;
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
@@ -965,10 +966,10 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
                         clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg);
+                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg, nsteps);
                     else
                         clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg);
+                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg, nsteps);
 #ifdef MCEIK_STEPSTATS
                     {   // experiment: visited blocks of this sweep that did not change
                         const int c1 = clock - L.infl;
@@ -1010,6 +1011,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                 atomicAdd(L.visit_stats + 2, (unsigned long long)(unsigned)S.scratch[3]);
 #else
                 atomicAdd(L.visit_stats + 2, (unsigned long long)nchg);
+                atomicAdd(L.visit_stats + 3, (unsigned long long)nsteps);
 #endif
 #endif
             }

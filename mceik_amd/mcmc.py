@@ -438,8 +438,9 @@ class Sampler:
 
     def fsm_stats(self, reset=False):
         """(FSM kernel ms from hipEvents, launches, executed iterations summed over
-        solves, (tile visits, column segments updated, segments changed))."""
-        ms, nl, it, tv = C.c_double(0), C.c_longlong(0), C.c_ulonglong(0), (C.c_ulonglong * 3)()
+        solves, (brick visits, column segments updated, segments changed, wave macro
+        steps))."""
+        ms, nl, it, tv = C.c_double(0), C.c_longlong(0), C.c_ulonglong(0), (C.c_ulonglong * 4)()
         if self._L.mceik_mcmc_fsm_stats(self._h, C.byref(ms), C.byref(nl), C.byref(it), tv, int(reset)) != 0:
             raise RuntimeError("mceik_mcmc_fsm_stats failed")
         return ms.value, nl.value, it.value, tuple(tv)
