@@ -1239,18 +1239,19 @@ static int pipes_setup(mceik_mcmc *s, int np)
 {
     const int nch = s->D.nchains;
     const size_t ncm = (size_t)s->D.ncm;
-    // the scratch budget binds (large grids): the pipes share the waves one
-    // pipe would keep, so every workspace together stays within the budget
+    // The scratch budget binds (large grids: fewer resident waves than the
+    // occupancy allows): pipes would have to share those waves, and splitting
+    // them lengthens each half's queue tail more than the other half fills
+    // (C5: 24.3 vs 25.1 proposals/s, profiles/r03_cfg): run one pipe.
     const int w1 = ws_layout(&s->fb).nwaves;
-    const bool capped = w1 < (long long)fsm_batch_waves_uncapped(&s->fb);
+    if (w1 < fsm_batch_waves_uncapped(&s->fb)) {
+        fprintf(stderr, "mceik_mcmc_init: the FSM scratch budget caps the waves (%d); running one pipe\n", w1);
+        return 0;
+    }
     for (int k = 0; k < np; k++) {
         const int lo = (int)((long long)nch * k / np), hi = (int)((long long)nch * (k + 1) / np);
         s->pD[k] = dev_view(s->D, lo, hi - lo);
         s->pfb[k] = batch_view(s->fb, lo, hi - lo, ncm);
-        if (capped) {
-            const int share = w1 / np > 0 ? w1 / np : 1;
-            if (s->pfb[k].max_waves <= 0 || s->pfb[k].max_waves > share) s->pfb[k].max_waves = share;
-        }
     }
     // workspaces: carved out of the sampler's own when they fit in it together
     // (budget-capped grids), else pipe 0 reuses it and the others get their own
