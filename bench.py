@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v27"          # bump when the sweep kernel changes; profiles/traffic.json must match
+KERNEL_REV = "fsm-v29"          # bump when the sweep kernel changes; profiles/traffic.json must match
 
 
 # ---------------------------------------------------------------- CPU baseline

@@ -122,6 +122,9 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 #ifndef MCEIK16_LEAN
 #define MCEIK16_LEAN 1           // the fixed instance decodes lean position words
 #endif
+#ifndef MCEIK16_HALOLINE
+#define MCEIK16_HALOLINE 1       // the fixed instance loads whole halo lines (with the lean words)
+#endif
 #ifndef MCEIK16_NPASS
 #define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
 #endif
@@ -469,6 +472,25 @@ __device__ __forceinline__ uint32_t halo_offset_lean(const Pos &pe, int nstream,
     const uint32_t o = base + ((me & hbit) ? 0u : hdelta) + ((uint32_t)(ph ^ (RZ ? 1 : 0)) << 6) + (uint32_t)half * 32u;
     return valid ? o : OOB;
 }
+// Whole-line halo loads (the fixed instance): the line base of halo column
+// j at the edge lane's position pe, valid when the position and either of
+// its bricks are.  Halo columns 2i and 2i+1 belong to edge lanes of adjacent
+// skews, so at every step exactly one of them targets the first brick of a
+// position: the four lanes of quad i then load that column's whole line (the
+// first brick staged at the end of the next step, the second one step
+// later), lane r taking quarter r of both halves.
+template <bool RZ>
+__device__ __forceinline__ uint32_t halo_line_lean(const Pos &pe, int nstream, unsigned me, uint32_t base,
+                                                   unsigned hbit, uint32_t hdelta)
+{
+    const bool valid = pos_valid(pe, nstream) && (me & ((16u << LW_G(0)) | (16u << LW_G(1))));
+    return valid ? base + ((me & hbit) ? 0u : hdelta) : OOB;
+}
+// lanes r <-> r ^ 2 within each quad (quad_perm 2, 3, 0, 1)
+__device__ __forceinline__ unsigned dpp_swap_quad_half(unsigned v)
+{
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+}
 // the brick info / halo offset of a step: lean (fixed instance) or general
 template <bool RZ, bool LEAN>
 __device__ __forceinline__ BInfo16 brick_info_any(const FsmLaunch &L, const Fsm16Geo &g, int kb, const Smem16 &S,
@@ -780,6 +802,16 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     LineLd lq;                                       // FL: this step's line loads
     float hps[2][8];                                 // FL: held line halves
     float (&hq)[8] = hs[0];                          // prologue names: halo of step 0, of step 1
+    // HFL (whole halo lines): quad i = halo columns 2i, 2i+1; column 2i + hfl(P)
+    // loads its line at steps of parity P (hpi: parity of column 2i's lag).
+    // hA[P]: the first brick loaded at a step of parity P, staged at the end
+    // of the next step; hB[P]: the second brick, staged two steps later (hBs
+    // holds it over the step that reloads hB[P])
+    constexpr bool HFL = FL && LEAN && MCEIK16_HALOLINE;
+    const int hr = lane & 3, hpi = (lane >> 4) & 1, hcme = (lane >> 1) & 1;
+    const int hj0 = (lane >> 1) & ~1;
+    const int hst = XROW16((hj0 >> 3) & 1, hr, 64 + ((hj0 >> 4) << 3) + (hj0 & 7));   // column 2i's row, quarter r
+    float hA[2][4], hB[2][4], hBs[4];
     float (&hn)[8] = hs[1];
     float (&hp)[8] = hps[0];
     float zc, zn, zq;
@@ -871,7 +903,22 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hp[i]));
     }
     pos_adv(pe, kb, nr);
-    {
+    if (HFL) {
+        // bricks vb = 1 - hd of both columns (staged at the end of step 0) and
+        // the second brick of the loader of parity 1 (staged at the end of
+        // step 1): the loader of parity 1 starts its line at 1 - hd, the one
+        // of parity 0 holds 1 - hd as its second brick.  Both positions are
+        // decided (vb <= 1).
+        const uint32_t lo = halo_line_lean<RZ>(pe, nstream, S.meta[pe.ri * 64 + he], S.ring_base[pe.ri] + hcol, hbit,
+                                               hdelta);
+        const uint32_t lp = dpp_swap_quad_half(lo);
+        const uint32_t l1 = hcme == (hpi ^ 1) ? lo : lp, l0 = hcme == hpi ? lo : lp;
+        const uint32_t qo = 16u * (uint32_t)hr, oa = (RZ ? 64u : 0u) + qo, ob = (RZ ? 0u : 64u) + qo;
+        bload4h(ur, l1 + oa, hA[1]);
+        bload4h(ur, l0 + ob, hB[0]);
+        bload4h(ur, l1 + ob, hB[1]);
+        TRAF(S, 1, l1 != OOB, 32);
+    } else {
         const uint32_t ho = halo_offset_any<RZ, LEAN>(g, kb, pe, nstream, hh, S.meta[pe.ri * 64 + he],
                                               S.ring_base[pe.ri] + hcol, hbit, hdelta);
         bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hn[0]));
@@ -891,12 +938,17 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     float zprev = UN;                                // last slot of the previous brick (sweep order)
     // the prologue's loads are waited for here, once per sweep; step 0 stages
     // hs[0] = the halos loaded second (hn)
+    if (HFL) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) hs[0][i] = hs[1][i];
+        for (int i = 0; i < 4; i++) asm volatile("" : "+v"(hA[1][i]), "+v"(hB[0][i]), "+v"(hB[1][i]));
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) hs[0][i] = hs[1][i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hs[0][i]));
+    }
 #pragma unroll
     for (int i = 0; i < 16; i++) asm volatile("" : "+v"(v[i]));
-#pragma unroll
-    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(hs[0][i]));
     asm volatile("" : "+v"(zc), "+v"(zn));
     asm volatile("" ::: "memory");
 
@@ -949,7 +1001,19 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         else
             seg_issue(ur, b3.seg, qa);
         zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
-        {
+        if (HFL) {
+            const uint32_t lo = halo_line_lean<RZ>(pe, nstream, me, ce, hbit, hdelta);
+            const uint32_t lp = dpp_swap_quad_half(lo);
+            const uint32_t sl = hcme == (hpi ^ P) ? lo : lp;         // this step's loader column's line
+            const uint32_t qo = 16u * (uint32_t)hr;
+#pragma unroll
+            for (int i = 0; i < 4; i++) hBs[i] = hB[P][i];
+            bload4h(ur, sl + (RZ ? 64u : 0u) + qo, hA[P]);
+            bload4h(ur, sl + (RZ ? 0u : 64u) + qo, hB[P]);
+            TRAF(S, 1, sl != OOB, 32);
+            TRAF(S, 0, b3.seg != OOB, 64);
+            TRAF(S, 2, b3.zh != OOB, 4);
+        } else {
             const uint32_t ho = halo_offset_any<RZ, LEAN>(g, kb, pe, nstream, hh, me, ce, hbit, hdelta);
             bload4h(ur, ho, *reinterpret_cast<float (*)[4]>(&hnew[0]));
             bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hnew[4]));
@@ -1009,7 +1073,16 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         } else {
             seg_finish(qa, nn);
         }
-        halo_stage16(S.xr, lane, hcur);
+        if (HFL) {
+            // the first brick loaded last step -> the other column (this
+            // step's non-loader), the second brick loaded two steps ago ->
+            // this step's loader column
+            const int lc = hpi ^ P;
+            lds_w4(S.xr + hst + 4 * (1 - lc), hA[1 - P][0], hA[1 - P][1], hA[1 - P][2], hA[1 - P][3]);
+            lds_w4(S.xr + hst + 4 * lc, hBs[0], hBs[1], hBs[2], hBs[3]);
+        } else {
+            halo_stage16(S.xr, lane, hcur);
+        }
         zc = zn; zn = zq;
         if (!FL) {
 #pragma unroll
@@ -1019,8 +1092,13 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
 #pragma unroll
             for (int i = 0; i < 8; i++) hcur[i] = hnew[i];
         }
-        asm volatile("" : "+v"(hnew[0]), "+v"(hnew[1]), "+v"(hnew[2]), "+v"(hnew[3]), "+v"(hnew[4]), "+v"(hnew[5]),
-                     "+v"(hnew[6]), "+v"(hnew[7]));
+        if (HFL) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) asm volatile("" : "+v"(hA[P][i]), "+v"(hB[P][i]));
+        } else {
+            asm volatile("" : "+v"(hnew[0]), "+v"(hnew[1]), "+v"(hnew[2]), "+v"(hnew[3]), "+v"(hnew[4]),
+                         "+v"(hnew[5]), "+v"(hnew[6]), "+v"(hnew[7]));
+        }
         asm volatile("" : "+v"(zn));
         asm volatile("" ::: "memory");
         // ---- rows for the next step: results (XR), then this lane's next
