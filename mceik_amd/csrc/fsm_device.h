@@ -307,7 +307,7 @@ __device__ __forceinline__ double godunov_v(double a, double b, double c, double
 
 // ---- per-solve setup: u = u_nan, then the source boxes (EIKONAL3D_SETBCS) ----
 template <typename R, int SLOWMODE>
-__device__ bool init_field(const FsmLaunch &L, R *u, Rsrc ur, const void *slow_model, const double *src,
+__device__ __forceinline__ bool init_field(const FsmLaunch &L, R *u, Rsrc ur, const void *slow_model, const double *src,
                            BcBoxes &bc)
 {
     const int lane = threadIdx.x;
@@ -393,7 +393,7 @@ __device__ __forceinline__ int next_solve(const FsmLaunch &L, int &pass)
 
 // Diagonal order of the tiles for the (+x, +y) sweep: by txs + tys, then tys.
 // Other directions flip tx / ty; every tile comes after its upwind neighbours.
-__device__ void build_order(const FsmLaunch &L, int *order)
+__device__ __forceinline__ void build_order(const FsmLaunch &L, int *order)
 {
     for (int id = threadIdx.x; id < L.ntiles; id += 64) {
         const int txs = id % L.ntx, tys = id / L.ntx, dg = txs + tys;

@@ -856,7 +856,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 // changed): the z-blocks that changed in this iteration (lastchg >= the
 // iteration's first clock); u0 was stored at their first visit.
 template <typename R>
-__device__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int clock_it, bool &notconv)
+__device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int clock_it, bool &notconv)
 {
     const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
     const R T = (R)L.conv_thresh, tolr = (R)L.tol;
