@@ -459,13 +459,21 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
     const R zprev = (fl & F_ZH) ? zc : r[RZ ? 0 : 7];
     // the four neighbour rows (sweep-relative lanes: -1 / -8 upwind in XR,
     // +1 / +8 downwind in XN; tile-edge lanes read the halo rows)
+    // fp64: each slot's four neighbours are read when the slot is updated (the
+    // four whole rows would hold 64 VGPRs for the brick)
+    constexpr bool LAZY = sizeof(R) == 8;
     R xmr[8], xpr[8], ymr[8], ypr[8];
-    {
-        const int lxs = lane & 7, lys = lane >> 3;
-        load_row(S.xr, XROW(0, 0, lxs > 0 ? lane - 1 : 64 + lys), xmr);
-        load_row(S.xr, XROW(0, 0, lys > 0 ? lane - 8 : 72 + lxs), ymr);
-        load_row(S.xr, XROW(1, 0, lxs < 7 ? lane + 1 : 64 + lys), xpr);
-        load_row(S.xr, XROW(1, 0, lys < 7 ? lane + 8 : 72 + lxs), ypr);
+    const int lxs = lane & 7, lys = lane >> 3;
+    const int oxm = XROW(0, 0, lxs > 0 ? lane - 1 : 64 + lys), oym = XROW(0, 0, lys > 0 ? lane - 8 : 72 + lxs);
+    const int oxp = XROW(1, 0, lxs < 7 ? lane + 1 : 64 + lys), oyp = XROW(1, 0, lys < 7 ? lane + 8 : 72 + lxs);
+    // fp64: the next brick's first slot from this lane's XN row (the sweep
+    // keeps no register copy of the next brick)
+    const R nfirst = LAZY ? S.xr[XROW(1, RZ ? 1 : 0, lane) + (RZ ? 3 : 0)] : n[RZ ? 7 : 0];
+    if (!LAZY) {
+        load_row(S.xr, oxm, xmr);
+        load_row(S.xr, oym, ymr);
+        load_row(S.xr, oxp, xpr);
+        load_row(S.xr, oyp, ypr);
     }
     // fast fp32 path over the LDS cell cache: f, f*f, 2f*f, 3f*f per cell
     constexpr bool CELLF = SLOWMODE == 2 && ZSH >= 0 && !GENERIC && sizeof(R) == 4;
@@ -476,6 +484,11 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
         const int pprev = RZ ? pj + 1 : pj - 1;
         const int pnext = RZ ? pj - 1 : pj + 1;
         const R self = c[pj];
+        if (LAZY) {
+            const int sl = (pj & 3) + (pj >> 2) * 4 * MCEIK_XROWS;
+            xmr[pj] = S.xr[oxm + sl]; ymr[pj] = S.xr[oym + sl];
+            xpr[pj] = S.xr[oxp + sl]; ypr[pj] = S.xr[oyp + sl];
+        }
         R ux, uy, fv;
         gather_xy<R, SLOWMODE, ZSH, GENERIC, !CELLF>(L, S, b0, c, xmr, xpr, ymr, ypr, pj, xp, xn, yp, yn, ux, uy, fv);
         if (CELLF) {
@@ -494,10 +507,10 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
             const bool zp_ex = RZ ? (zabs < L.nz - 1) : (zabs > 0);
             const bool zn_ex = RZ ? (zabs > 0) : (zabs < L.nz - 1);
             zup = zp_ex ? (j > 0 ? r[pprev] : zprev) : self;
-            zdn = zn_ex ? (j < 7 ? c[pnext] : n[RZ ? 7 : 0]) : self;
+            zdn = zn_ex ? (j < 7 ? c[pnext] : nfirst) : self;
         } else {
             zup = j > 0 ? r[pprev] : (first ? self : zprev);
-            zdn = j < 7 ? c[pnext] : (last ? self : n[RZ ? 7 : 0]);
+            zdn = j < 7 ? c[pnext] : (last ? self : nfirst);
         }
         const R uz = fmin_(zup, zdn);
         R nv;
@@ -769,8 +782,22 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 if (AH == 3) q[i] = p[i];
             }
         }
+        // u0: a block's first visit in the iteration (old values c)
+        auto u0_store = [&]() __attribute__((always_inline)) {
+            if (!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) {
+                R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
+                const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
+                if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
+                TRAF(S, 4, st0, 8 * sizeof(R));
+            }
+        };
         // neighbour rows for the next step: this step's results, the next brick
+        // (fp64: the brick of the next step is read back from the XN row first,
+        // so c's u0 copy is stored before)
+        constexpr bool LAZYN = sizeof(R) == 8 && !ROT;
+        if (LAZYN) u0_store();
         store_row(S.xr, 0, lane, r);
+        if (LAZYN) load_row(S.xr, XROW(1, 0, lane), c);
         store_row(S.xr, 1, lane, nn);
         if (!ROT) {
 #pragma unroll
@@ -794,18 +821,14 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 bstore8(ur, changed ? b0.seg : OOB, r);
             TRAF(S, 3, changed, 8 * sizeof(R));
         }
-        if (!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) {      // a block's first visit in the iteration
-            R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
-            const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
-            if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
-            TRAF(S, 4, st0, 8 * sizeof(R));
-        }
+        if (!LAZYN) u0_store();
         if (changed) S.lastchg[b0.bid] = clock0 + b0.clk;   // lanes of one block write the same value
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             if (ROT) {
                 c[i] = nn[i];            // c's registers become the next step's n
+            } else if (LAZYN) {
             } else {
                 c[i] = n[i];
                 n[i] = nn[i];
@@ -892,7 +915,9 @@ __device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u
 #ifdef MCEIK_WPE
 #define FSM_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE, MCEIK_WPE)))
 #else
-#define FSM_WPE
+// fp64: two waves per SIMD (the register budget that allows it: 4 B of
+// spills outside the step loop, against one wave with AGPR spills)
+#define FSM_WPE __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 ? 2 : 1)))
 #endif
 template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)

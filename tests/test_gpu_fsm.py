@@ -146,6 +146,66 @@ def test_fp32_inversion_grid_mode_bitwise(fast, nz):
         assert int(out["niter"][s]) == it
 
 
+FP64_CASES = [c for c in CASES if c[0] in ("hetero_16^3_top", "rough_24x20x16_onnode", "rough_13x9x11_xmax",
+                                           "hetero_21x18x15_2src", "rough_9x10x8_loose", "hetero_40x33x90_deep",
+                                           "hetero_33x41x25_maxit2")]
+
+
+@pytest.mark.parametrize("case", FP64_CASES, ids=[c[0] for c in FP64_CASES])
+def test_fp64_batch_bitwise_vs_oracle(case):
+    """The batched fp64 kernel (per-node slowness, the reference's literal
+    update, fsm3d.f90:562-693): fields bitwise = the fp64 oracle (itself
+    bitwise = the reference on tests/golden), iterations and ierr equal."""
+    name, nx, ny, nz, kind, srcs, maxit, tol = case
+    dev = _dev()
+    h = 100.0
+    slow64 = _case_slow(kind, nx, ny, nz)
+    src = np.asarray(srcs, dtype=np.float64)
+    bs = _solver(nx, ny, nz, h, 64, maxit, tol)
+    out = bs.solve(torch.tensor(src[None]), torch.tensor(slow64.reshape(1, nz, ny, nx), device=dev),
+                   want_fields=True)
+    g = out["u"].cpu().numpy().ravel()
+    t, ierr, it = O.eikonal_solve(nx, ny, nz, slow64, h, src, maxit=maxit, tol=tol)
+    assert np.array_equal(g.view(np.uint64), t.view(np.uint64)), name
+    assert int(out["niter"][0]) == it
+    assert int(out["ierr"][0]) == ierr
+
+
+@pytest.mark.parametrize("nz,max_waves", [(34, 0), (67, 2)], ids=["kb4", "kb4_ragged_reuse"])
+def test_fp64_inversion_grid_mode_bitwise(nz, max_waves):
+    """The fp64 sampler's kernel (bench.py --precision 64): per-cell fp32
+    slowness, fp64 fields and the literal update.  Several models and stations
+    per launch (max_waves 2: several solves per wave in reused scratch);
+    fields, event tables, iterations bitwise = the fp64 oracle on the expanded
+    field."""
+    dev = _dev()
+    nx, ny, h, nref = 30, 26, 100.0, (4, 4, 4)
+    ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
+    rng = np.random.default_rng(23)
+    nmodel = 2
+    v = rng.integers(2500, 6500, (nmodel, ncz, ncy, ncx)).astype(np.int32)
+    scell = (1.0 / v.astype(np.float32)).astype(np.float32)
+    k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    src = np.array([[[0.0, 1234.5, 987.6, (nz - 1) * h]], [[0.0, 300.0, 2200.0, (nz - 1) * h]],
+                    [[0.1, 1500.0, 1200.0, 1700.0]]])
+    ev = rng.integers(0, nx * ny * nz, 7).astype(np.int32)
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 64, nref=nref)
+    out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(nmodel, -1), device=dev),
+                   ev_node=torch.tensor(ev), want_fields=True, max_waves=max_waves)
+    assert out["step_z"] == 8
+    u = out["u"].cpu().numpy().reshape(nmodel * len(src), -1)
+    tt = out["ttab"].cpu().numpy()
+    for m in range(nmodel):
+        sfield = scell[m][k // nref[2], j // nref[1], i // nref[0]].ravel().astype(np.float64)
+        for s in range(len(src)):
+            t, ierr, it = O.eikonal_solve(nx, ny, nz, sfield, h, src[s])
+            q = m * len(src) + s
+            assert np.array_equal(u[q].view(np.uint64), t.view(np.uint64)), (m, s)
+            assert np.array_equal(tt[q].view(np.uint32), t[ev].astype(np.float32).view(np.uint32)), (m, s)
+            assert int(out["niter"][q]) == it and int(out["ierr"][q]) == ierr
+
+
 def test_solve_order_and_clock():
     """A permuted work order (mceik_fsm_batch.solve_order) gives bitwise the
     same fields, tables and iteration counts; solve_clock stamps every solve."""
