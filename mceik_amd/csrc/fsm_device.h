@@ -302,7 +302,7 @@ template <bool FAST>
 __device__ __forceinline__ double godunov_v(double a, double b, double c, double f, double, double, double)
 {
     int e;
-    return godunov(a, b, c, f, e);
+    return MCEIK_F64_SELECT ? godunov_sel(a, b, c, f, e) : godunov(a, b, c, f, e);
 }
 
 // ---- per-solve setup: u = u_nan, then the source boxes (EIKONAL3D_SETBCS) ----

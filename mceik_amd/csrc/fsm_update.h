@@ -57,6 +57,37 @@ __device__ __forceinline__ double godunov(double a, double b, double c, double f
     return UN;
 }
 
+// The same update without branches (MCEIK_F64_SELECT): the sorted triple by
+// min / max / median, the 1D, 2D and 3D candidates all computed, the
+// reference's choice made by selects.  Values and ierr identical to godunov()
+// (inputs are never NaN; a root of a negative radicand is NaN only in a
+// candidate that is not selected, or gives the reference's ierr 3).  A wave
+// whose lanes take different branches runs every branch anyway; this form
+// drops the exec-mask bookkeeping and branches of the divergent code.
+#ifndef MCEIK_F64_SELECT
+#define MCEIK_F64_SELECT 1
+#endif
+__device__ __forceinline__ double godunov_sel(double a, double b, double c, double f, int &ierr)
+{
+    const double UN = DBL_MAX;
+    const double a1 = __builtin_fmin(__builtin_fmin(a, b), c);
+    const double a3 = __builtin_fmax(__builtin_fmax(a, b), c);
+    const double a2 = __builtin_fmax(__builtin_fmin(a, b), __builtin_fmin(__builtin_fmax(a, b), c));
+    const double x1 = a1 + f;
+    const double amb = a1 - a2;
+    const double arg = (2.0 * f) * f - amb * amb;
+    const double x2 = __builtin_fabs(amb) < f ? 0.5 * ((a1 + a2) + __builtin_sqrt(arg)) : (a1 < a2 ? a1 : a2) + f;
+    const double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
+    const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
+    const double disc = qb * qb - 4.0 * qc;
+    const double x3 = 0.5 * (-qb + __builtin_sqrt(disc));
+    const bool in3 = x3 < UN;
+    const bool r1 = !(x1 > a2), r2 = !(x2 > a3), nan_in = a1 == UN;
+    const int e3 = in3 ? (x3 < 0.0 ? 2 : (disc < 0.0 ? 1 : 0)) : 3;
+    ierr = (nan_in || r1 || r2) ? 0 : e3;
+    return nan_in ? UN : r1 ? x1 : r2 ? x2 : (in3 ? x3 : UN);
+}
+
 // Correctly rounded sqrt for normal positive x (LLVM's expansion without the
 // denormal rescale and zero/inf fix-up).  Used only where the radicand that
 // is finally selected is provably a normal float: on the MCMC path f = h*s >=
@@ -125,7 +156,7 @@ __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, 
 template <bool FAST>
 __device__ __forceinline__ double godunov_bl(double a, double b, double c, double f, int &ierr)
 {
-    return godunov(a, b, c, f, ierr);   // fp64: the reference's literal form
+    return MCEIK_F64_SELECT ? godunov_sel(a, b, c, f, ierr) : godunov(a, b, c, f, ierr);   // fp64: literal form
 }
 
 // min of two travel times.  Values in the field are never NaN or -0 (every
