@@ -82,7 +82,8 @@ class McmcInfo(C.Structure):
     """mceik_mcmc_info (include/mceik.h)."""
     _fields_ = [("npipe", C.c_int), ("nphase", C.c_int), ("step_z", C.c_int), ("fixed_layout", C.c_int),
                 ("chains", C.c_int * 4), ("waves", C.c_int * 4), ("workspace_bytes", C.c_size_t * 4),
-                ("lds_bytes", C.c_size_t), ("masked_s", C.c_int), ("kernel", C.c_char * 64)]
+                ("lds_bytes", C.c_size_t), ("masked_s", C.c_int), ("kernel", C.c_char * 64),
+                ("multi_step", C.c_int)]
 
 
 # every extern "C" symbol include/*.h declares

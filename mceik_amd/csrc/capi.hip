@@ -250,8 +250,25 @@ extern "C" double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b)
     return 2.0 * es + s / (b->nstat > 0 ? b->nstat : 1);
 }
 
+// The sampler's multi-step launch (FsmLaunch mc_*): not part of the public batch.
+#define MCEIK_MC_CHUNK 64        // steps per multi-step launch (bounds one kernel's duration)
+struct McmcExt {
+    const void *dev;             // device copy of the sampler's McmcDev
+    unsigned *sync;              // MC_SYNC_WORDS(nchains) words, zeroed here before the launch
+    int step0, nsteps, nburn, keepk, maxs, nkept0;
+};
+
+static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes, void *stream,
+                                const McmcExt *ext);
+
 extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes,
                                      void *stream)
+{
+    return fsm_batch_solve_impl(b, workspace, workspace_bytes, stream, nullptr);
+}
+
+static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_t workspace_bytes, void *stream,
+                                const McmcExt *ext)
 {
     if (!b || b->nx < 2 || b->ny < 2 || b->nz < 2 || b->nx > 4096 || b->ny > 4096 || b->nz > 4096 ||
         b->nsrc < 1 ||
@@ -298,6 +315,14 @@ extern "C" int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, 
     L.u = ws + w.u;
     L.u0 = ws + w.u0;
     L.slot_per_solve = b->u_out ? 1 : 0;
+    if (ext) {
+        if (is_double || fsm_launch_kind(L, 0) != 16 || b->solve_order || b->u_out) return 1;
+        L.mc_dev = ext->dev;
+        L.mc_sync = ext->sync;
+        L.mc_step0 = ext->step0; L.mc_nsteps = ext->nsteps;
+        L.mc_nburn = ext->nburn; L.mc_keepk = ext->keepk; L.mc_maxs = ext->maxs; L.mc_nkept0 = ext->nkept0;
+        HIPCHK(fsm_zero_words(ext->sync, MC_SYNC_WORDS(L.nsolve / L.nstat), st));
+    }
     HIPCHK(fsm_launch(L, is_double, w.nwaves, st));
     if (b->u_out) {
         if (is_double) HIPCHK(fsm_from_brick_f64(L.u, 1, (double *)b->u_out, L, L.nsolve, st));
@@ -1043,6 +1068,14 @@ struct mceik_mcmc {
     // half's queue tail leaves idle.  Results are those of
     // one pipe bit for bit.
     int npipe;
+    // Multi-step launches (MCEIK_PERSIST=1, where the 16-z kernel runs): one
+    // FSM launch runs up to MCEIK_MC_CHUNK steps, the
+    // chain epilogue (accept, kept state, next proposal) inside the kernel
+    // (fsm16_kernel.hip mc_finish), so no step waits for the slowest chain of
+    // the one before.  d_dev: device copy of D; d_sync: the launch's queues.
+    bool persist;
+    McmcDev *d_dev;
+    unsigned *d_sync;
     hipStream_t pst[MCEIK_MAX_PIPES];
     hipEvent_t pfork, pjoin[MCEIK_MAX_PIPES];
     McmcDev pD[MCEIK_MAX_PIPES];
@@ -1132,7 +1165,7 @@ static int fold_launch(mceik_mcmc *s, long long k)
     return 0;
 }
 
-static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
+static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1, const McmcExt *ext = nullptr)
 {
     mceik_fsm_batch &fb = pipe < 0 ? s->fb : s->pfb[pipe];
     void *ws = pipe >= 0 ? s->pws[pipe] : s->ws;
@@ -1153,7 +1186,7 @@ static int mcmc_forward(mceik_mcmc *s, bool timed, int pipe = -1)
         }
         HIPCHK(hipEventRecord(s->ev[2 * r], st));
     }
-    if (mceik_fsm_batch_solve(&fb, ws, ws_bytes, st)) return -1;
+    if (fsm_batch_solve_impl(&fb, ws, ws_bytes, st, ext)) return -1;
     s->last_ttab = s->fb.ttab;
     if (timed) {
         HIPCHK(hipEventRecord(s->ev[2 * r + 1], st));
@@ -1547,8 +1580,16 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     s->report = report;
     if (report) clock_report(s, "init");
     s->npipe = 1;
+    // MCEIK_PERSIST=1: multi-step launches where eligible (measured slower than
+    // two pipes at C3, DESIGN.md s.3.5, so off by default)
+    const char *persist_env = getenv("MCEIK_PERSIST");
+    s->persist = persist_env && persist_env[0] == '1' && b.precision == 32 && mceik_fsm_step_z(&b) == 16 && !lpt;
+    if (s->persist && (dalloc(s, &s->d_sync, MC_SYNC_WORDS(nch)) || dput(s, &s->d_dev, &D, 1))) {
+        mceik_mcmc_finalize(&s);
+        return -1;
+    }
     const char *pipe_env = getenv("MCEIK_PIPES");       // default 2; MCEIK_PIPES=1: one pipe
-    int np = pipe_env ? atoi(pipe_env) : 2;
+    int np = s->persist ? 1 : pipe_env ? atoi(pipe_env) : 2;
     np = np < 1 ? 1 : np > MCEIK_MAX_PIPES ? MCEIK_MAX_PIPES : np;
     if (np > nch) np = nch;
     if (np > 1 && pipes_setup(s, np)) {
@@ -1572,6 +1613,24 @@ extern "C" int mceik_mcmc_set_stream(mceik_mcmc *s, void *stream)
 // kernel this call queued on the internal streams.
 static int mcmc_steps(mceik_mcmc *s, int nsteps)
 {
+    if (s->persist) {
+        // the first step's proposals here, then up to MCEIK_MC_CHUNK steps per
+        // FSM launch (the kernel accepts, keeps and proposes the rest)
+        for (int done = 0; done < nsteps;) {
+            const int n = std::min(nsteps - done, MCEIK_MC_CHUNK);
+            McmcExt x;
+            x.dev = s->d_dev; x.sync = s->d_sync;
+            x.step0 = (int)s->step; x.nsteps = n;
+            x.nburn = s->nburn; x.keepk = s->keepk; x.maxs = s->max_samples; x.nkept0 = s->nkept;
+            HIPCHK(mcmc_propose(s->D, (uint64_t)s->step, s->stream));
+            if (mcmc_forward(s, true, -1, &x)) return -1;
+            for (int i = 0; i < n; i++, s->step++)
+                if (s->max_samples && s->step >= s->nburn && (s->step - s->nburn) % s->keepk == 0) s->nkept++;
+            if (s->report) clock_report(s, "steps");
+            done += n;
+        }
+        return 0;
+    }
     const int np = s->npipe;
     for (int i = 0; i < nsteps; i++) {
         uint64_t step = (uint64_t)s->step;
@@ -1765,6 +1824,7 @@ extern "C" int mceik_mcmc_get_info(mceik_mcmc *s, mceik_mcmc_info *info)
     DeviceScope dg(s->device);
     memset(info, 0, sizeof(*info));
     info->npipe = s->npipe;
+    info->multi_step = s->persist ? 1 : 0;
     info->nphase = s->D.nphase;
     info->masked_s = s->masked_s;
     FsmLaunch L;

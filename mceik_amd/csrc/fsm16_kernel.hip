@@ -27,6 +27,7 @@
 #include "fsm_common.h"
 #include "fsm_device.h"
 #include "fsm_update.h"
+#include "mcmc_device.h"
 
 namespace {
 
@@ -510,7 +511,7 @@ __device__ __forceinline__ uint32_t halo_offset_any(const Fsm16Geo &g, int kb, c
 
 // Diagonal order of the tiles for the (+x, +y) sweep (build_order in
 // fsm_device.h, 16-bit entries txs | tys << 8).
-__device__ void build_order16(const FsmLaunch &L, unsigned short *order)
+__device__ __forceinline__ void build_order16(const FsmLaunch &L, unsigned short *order)
 {
     for (int id = threadIdx.x; id < L.ntiles; id += 64) {
         const int txs = id % L.ntx, tys = id / L.ntx, dg = txs + tys;
@@ -641,7 +642,7 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
 // are those of unbounded clocks (all that matters of the past is the
 // pending state; nothing is in flight across an iteration boundary), and an
 // iteration needs at most 8 (nblocks (1 + vis) + infl) + 64 < 2^16 clocks.
-__device__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
+__device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
 {
     const int nt = L.ntiles, nzk = L.nzk;
     unsigned pend = 0;                       // bit i: block lane + 64 i (nblocks <= 1024)
@@ -1150,7 +1151,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
 // End-of-iteration check of the nodes below T (only when no node >= T
 // changed): the z-blocks changed in this iteration; u0 was stored at their
 // first visit (fsm_kernel.hip verify_small, 16-bit clocks).
-__device__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem16 &S, bool &notconv)
+__device__ __forceinline__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem16 &S, bool &notconv)
 {
     const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
     const float T = (float)L.conv_thresh, tolr = (float)L.tol;
@@ -1183,7 +1184,160 @@ __device__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem16 &S,
     }
 }
 
-template <int KB16, int CCR>
+// ---- multi-step sampler launch (L.mc_dev) ----------------------------------
+// The solves of mc_nsteps sampler steps in one launch, without a barrier
+// between steps: the chains are split into 8 groups, each group's solves of
+// all steps handed out by its own ticket counter in step-major, chain-major
+// order.  A chain's solves of step k wait until its step k - 1 is accepted
+// and step k proposed; the wave that completes the chain's last solve of a
+// step does both (mcmc_device.h: the per-step kernels' arithmetic, so the
+// results equal the step-by-step launches bit for bit).
+//
+// Coherence: hipMalloc memory is coherent within one XCD's L2 only, so a
+// group is owned by one XCD (the first that claims it: XCD id + 1 by CAS)
+// and only that XCD's waves serve it; a chain's solves, tables, state and
+// proposal then stay behind one L2.  Writers wait for their stores
+// (s_waitcnt) before the L2 atomics that publish them; readers invalidate
+// their CU's L1 (buffer_inv sc1) after observing them and load chain state
+// through vector loads (mcmcd::ldv).  A wave first serves its own XCD's
+// group, then any group its XCD owns or can claim, and exits when none has
+// tickets left, so every group is served whatever the XCD ids.  A ticket
+// only waits on earlier tickets of its own group, all held by running
+// waves: no deadlock, whatever the residency.
+struct McQueue {
+    unsigned xcc;                // this wave's XCD id + 1
+    int cur;                     // group being served, -1 none
+};
+__device__ __forceinline__ unsigned mc_group_tickets(const FsmLaunch &L, int g, int &clo)
+{
+    const int nch = L.nsolve / L.nstat;
+    clo = (int)((long long)nch * g / 8);
+    const int chi = (int)((long long)nch * (g + 1) / 8);
+    return (unsigned)(chi - clo) * (unsigned)L.nstat;
+}
+// (sc1: the agent-scope acquire's invalidate, which is what reaches the CU's
+// L1 -- workgroup scope (sc0) leaves a non-split workgroup's L1 alone; local
+// memory's L2 lines are not dropped by it)
+#ifndef MCEIK_MC_INV
+#define MCEIK_MC_INV "buffer_inv sc1"
+#endif
+__device__ __forceinline__ void mc_l1_invalidate()
+{
+    asm volatile(MCEIK_MC_INV "\n\ts_waitcnt vmcnt(0)" ::: "memory");
+}
+// every store issued so far has completed (reached L2) before what follows
+// is issued (the asm is also a compiler barrier: no store sinks past it)
+__device__ __forceinline__ void mc_stores_done()
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ bool mc_next(const FsmLaunch &L, McQueue &q, int &solve, int &k)
+{
+    const int lane = threadIdx.x;
+    unsigned *owner = L.mc_sync, *tick = L.mc_sync + 8;
+    int *ready = reinterpret_cast<int *>(L.mc_sync + 8 + 8 * 32);
+    for (;;) {
+        if (q.cur >= 0) {
+            int clo;
+            const unsigned gs = mc_group_tickets(L, q.cur, clo), tot = gs * (unsigned)L.mc_nsteps;
+            unsigned t = 0;
+            if (lane == 0) t = atomicAdd(tick + 32 * q.cur, 1u);
+            t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+            if (t < tot) {
+                k = (int)(t / gs);
+                solve = clo * L.nstat + (int)(t - (unsigned)k * gs);
+                const int c = solve / L.nstat;
+                if (lane == 0) {
+                    // (a safety net, never expected: after ~30 s the wave stops
+                    // waiting, so a broken queue ends the launch instead of
+                    // hanging the GPU; the sync buffer's last word says so)
+                    for (unsigned it = 0; atomicAdd(ready + c, 0) < k; it++) {
+                        if (it == (1u << 24)) {
+                            atomicExch(L.mc_sync + MC_SYNC_WORDS(L.nsolve / L.nstat) - 1, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(32);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                mc_l1_invalidate();
+                return true;
+            }
+            q.cur = -1;
+        }
+        int found = -1;
+        for (int j = 0; j < 8 && found < 0; j++) {
+            const int g = (int)((q.xcc - 1u + (unsigned)j) & 7u);
+            unsigned own = 0, left = 0;
+            if (lane == 0) {
+                own = atomicCAS(owner + g, 0u, q.xcc);
+                if (own == 0u) own = q.xcc;
+                int clo;
+                const unsigned tot = mc_group_tickets(L, g, clo) * (unsigned)L.mc_nsteps;
+                left = own == q.xcc && atomicAdd(tick + 32 * g, 0u) < tot ? 1u : 0u;
+            }
+            left = __builtin_amdgcn_readfirstlane(__shfl(left, 0, 64));
+            if (left) found = g;
+        }
+        if (found < 0) return false;
+        q.cur = found;
+    }
+}
+// kept-state slot of global step gs (mceik_mcmc_run's rule), or -1
+__device__ __forceinline__ int mc_keep_slot(const FsmLaunch &L, long long gs)
+{
+    if (!L.mc_maxs || gs < L.mc_nburn || (gs - L.mc_nburn) % L.mc_keepk) return -1;
+    auto nk = [&](long long x) -> long long {       // kept steps in [0, x)
+        return x <= L.mc_nburn ? 0 : (x - L.mc_nburn + L.mc_keepk - 1) / L.mc_keepk;
+    };
+    return (int)((L.mc_nkept0 + nk(gs) - nk(L.mc_step0)) % L.mc_maxs);
+}
+// After solve (c, station) of launch step k wrote its tables: count it; the
+// chain's last solve of the step runs the chain's accept (step mc_step0 + k),
+// kept state and next proposal, then marks step k + 1 ready.
+__device__ __forceinline__ void mc_finish(const FsmLaunch &L, int solve, int k)
+{
+    const int lane = threadIdx.x;
+    const int nch = L.nsolve / L.nstat, c = solve / L.nstat;
+    int *ready = reinterpret_cast<int *>(L.mc_sync + 8 + 8 * 32);
+    unsigned *done = L.mc_sync + 8 + 8 * 32 + nch;
+    mc_stores_done();                               // this solve's tables are in L2
+    unsigned old = 0;
+    if (lane == 0) old = atomicAdd(done + c, 1u);
+    old = __builtin_amdgcn_readfirstlane(__shfl(old, 0, 64));
+    if (old + 1u != (unsigned)(k + 1) * (unsigned)L.nstat) return;
+    mc_l1_invalidate();
+    const McmcDev &D = *reinterpret_cast<const McmcDev *>(L.mc_dev);
+    const long long gstep = (long long)L.mc_step0 + k;
+    const int keep_slot = mc_keep_slot(L, gstep);
+    // the proposal's logL: objfn of event e on lane e % 64, summed in event order
+    const int inp = mcmcd::ldv(&D.prop_inprior[c]), ph = mcmcd::ldv(&D.prop_phase[c]);
+    double ln = 0.0;
+    if (inp) {
+        for (int e0 = 0; e0 < D.nev; e0 += 64) {
+            const int e = e0 + lane, n = min(64, D.nev - e0);
+            const double obj = e < D.nev ? mcmcd::event_obj(D, c, ph, e) : 0.0;
+            for (int i = 0; i < n; i++) ln = ln - __shfl(obj, i, 64);
+        }
+    }
+    int acc = 0;
+    if (lane == 0) acc = mcmcd::chain_accept(D, c, ln, keep_slot);
+    acc = __builtin_amdgcn_readfirstlane(__shfl(acc, 0, 64));
+    if (acc && D.nphase > 1) mcmcd::chain_copy_tables(D, c, ph, lane, 64);
+    if (keep_slot >= 0) {                           // keep_kernel's copy of this chain (after the accept)
+        const int cell = mcmcd::ldv(&D.prop_cell[c]), pv = mcmcd::ldv(&D.prop_v[c]);
+        int *dst = D.keep_v + ((size_t)keep_slot * D.keep_stride + c) * D.ncm;
+        const int *src = D.v + (size_t)c * D.ncm;
+        for (int j = lane; j < D.ncm; j += 64) dst[j] = (acc && j == cell) ? pv : mcmcd::ldv(src + j);
+    }
+    if (k + 1 < L.mc_nsteps && lane == 0) mcmcd::chain_propose(D, c, (uint64_t)(gstep + 1));
+    mc_stores_done();                               // the chain's new state is in L2
+    if (lane == 0) atomicExch(ready + c, k + 1);
+}
+
+// MC: the multi-step sampler instance (L.mc_dev set); the plain batch
+// instances carry none of its code
+template <int KB16, int CCR, bool MC>
 __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1193,9 +1347,22 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
     const uint32_t fbytes = (uint32_t)(L.field_elems * 4);
     build_order16(L, S.order);
     int pass = 0;
+    McQueue mq;
+    mq.cur = -1;
+    mq.xcc = 1u;
+    if (MC) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        mq.xcc = (x & 0xfu) + 1u;
+    }
     for (;;) {
-        const int snext = next_solve(L, pass);
-        if (snext < 0) break;
+        int snext, mk = 0;
+        if (MC) {
+            if (!mc_next(L, mq, snext, mk)) break;
+        } else {
+            snext = next_solve(L, pass);
+            if (snext < 0) break;
+        }
         const unsigned solve = (unsigned)snext;
         if (L.solve_clock && lane == 0) L.solve_clock[2 * (size_t)solve] = __builtin_amdgcn_s_memrealtime();
         const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
@@ -1203,7 +1370,11 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         float *u = reinterpret_cast<float *>(L.u) + slot * L.field_elems;
         float *u0 = reinterpret_cast<float *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
         const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
-        const void *slow_model = reinterpret_cast<const float *>(L.slow) + fsm_slow_entry(L, model) * ncell;
+        // (a multi-step launch's model phase changes between steps: vector load)
+        const size_t sentry = !L.model_phase ? (size_t)model
+                                             : (size_t)model * L.nphase +
+                                                   (MC ? mcmcd::ldv(L.model_phase + model) : L.model_phase[model]);
+        const void *slow_model = reinterpret_cast<const float *>(L.slow) + sentry * ncell;
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
                    sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
         // Before the first sweep every block counts as visited and unchanged
@@ -1285,6 +1456,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         if (L.ttab) {
             for (int e = lane; e < L.nev; e += 64) L.ttab[(size_t)solve * L.nev + e] = event_time<float>(L, u, e);
         }
+        if (MC) mc_finish(L, (int)solve, mk);
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
@@ -1295,10 +1467,10 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
 #define MCEIK_WPE16 2
 #endif
 #define FSM16_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE16, MCEIK_WPE16)))
-template <int KB16, int CCR>
+template <int KB16, int CCR, bool MC>
 __global__ __launch_bounds__(64) FSM16_WPE void fsm16_solve_kernel(FsmLaunch L)
 {
-    fsm16_body<KB16, CCR>(L);
+    fsm16_body<KB16, CCR, MC>(L);
 }
 
 }  // namespace
@@ -1310,12 +1482,17 @@ hipError_t fsm16_launch(const FsmLaunch &L, int nwaves, hipStream_t st)
 {
     if (!fsm16_eligible(L, 4)) return hipErrorInvalidValue;
     const size_t lds = fsm16_lds_bytes(L);
-    if (fsm16_fixed_layout(L))
-        hipLaunchKernelGGL((fsm16_solve_kernel<2, 1>), dim3(nwaves), dim3(64), lds, st, L);
-    else if (L.ccb <= 64)
-        hipLaunchKernelGGL((fsm16_solve_kernel<0, 1>), dim3(nwaves), dim3(64), lds, st, L);
-    else
-        hipLaunchKernelGGL((fsm16_solve_kernel<0, 4>), dim3(nwaves), dim3(64), lds, st, L);
+    const bool mc = L.mc_dev != nullptr;
+    if (fsm16_fixed_layout(L)) {
+        if (mc) hipLaunchKernelGGL((fsm16_solve_kernel<2, 1, true>), dim3(nwaves), dim3(64), lds, st, L);
+        else hipLaunchKernelGGL((fsm16_solve_kernel<2, 1, false>), dim3(nwaves), dim3(64), lds, st, L);
+    } else if (L.ccb <= 64) {
+        if (mc) hipLaunchKernelGGL((fsm16_solve_kernel<0, 1, true>), dim3(nwaves), dim3(64), lds, st, L);
+        else hipLaunchKernelGGL((fsm16_solve_kernel<0, 1, false>), dim3(nwaves), dim3(64), lds, st, L);
+    } else {
+        if (mc) hipLaunchKernelGGL((fsm16_solve_kernel<0, 4, true>), dim3(nwaves), dim3(64), lds, st, L);
+        else hipLaunchKernelGGL((fsm16_solve_kernel<0, 4, false>), dim3(nwaves), dim3(64), lds, st, L);
+    }
     return hipGetLastError();
 }
 
@@ -1325,10 +1502,10 @@ int fsm16_occupancy(const FsmLaunch &L)
     const size_t lds = fsm16_lds_bytes(L);
     hipError_t e;
     if (fsm16_fixed_layout(L))
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<2, 1>, 64, lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<2, 1, false>, 64, lds);
     else if (L.ccb <= 64)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0, 1>, 64, lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0, 1, false>, 64, lds);
     else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0, 4>, 64, lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fsm16_solve_kernel<0, 4, false>, 64, lds);
     return e == hipSuccess ? nb : 1;
 }

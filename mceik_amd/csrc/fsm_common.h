@@ -57,7 +57,18 @@ struct FsmLaunch {
     const float *ev_frac;        // [nev][3] trilinear fractions (ev_node = lowest corner), or null = node value
     const int *model_phase;      // slow_mode 1: model m uses slow entry m * nphase + model_phase[m], or null
     int nphase;
+    // Multi-step sampler launch (fsm16 kernel only; null mc_dev: a plain
+    // batch).  Solves of steps mc_step0 .. mc_step0 + mc_nsteps - 1; the wave
+    // that completes a chain's solves of a step runs the chain's accept, kept
+    // state and next proposal (mcmc_device.h).  mc_sync: [8] group owner (XCD
+    // id + 1) | [8][32] group tickets | [nchains] steps ready | [nchains]
+    // solves done | [1] broken-queue flag, zeroed before the launch.
+    const void *mc_dev;          // the sampler's McmcDev (device copy)
+    unsigned *mc_sync;
+    int mc_step0, mc_nsteps;
+    int mc_nburn, mc_keepk, mc_maxs, mc_nkept0;   // kept-state slots (mceik_mcmc_run's bookkeeping)
 };
+#define MC_SYNC_WORDS(nchains) (8 + 8 * 32 + 2 * (nchains) + 1)
 
 // Inversion-grid slowness entry of model m (slow_mode 1).
 static inline __host__ __device__ size_t fsm_slow_entry(const FsmLaunch &L, int m)

@@ -235,7 +235,10 @@ __device__ __forceinline__ double slow_at(const FsmLaunch &L, const void *slow_m
 {
     if (SLOWMODE == 0)
         return (double)reinterpret_cast<const R *>(slow_model)[brick_index<R>(L, x, y, z)];   // modes 1, 2: cells
+    // (a vector load: the sampler's multi-step launch changes the cells between
+    // solves, and a wave-uniform address would make this a scalar-cache load)
     const float *si = reinterpret_cast<const float *>(slow_model);
+    asm volatile("" : "+v"(si));
     return (double)si[((size_t)(z / L.nrz) * L.ncy + y / L.nry) * L.ncx + x / L.nrx];
 }
 

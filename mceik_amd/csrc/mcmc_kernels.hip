@@ -1,147 +1,41 @@
 // mcmc_kernels.hip -- proposal, L2 misfit + Metropolis, and the L2 grid
 // search, on gfx950.
 //
-// The reference defines no MCMC (include/mceik.h:1-14 is empty; only
-// mcmc_parms_struct, mceik_struct.h:54-60).  The definition used here
-//  is restated on the CPU in oracle/mceik_oracle.c and the two
-// agree bit for bit: integer Philox4x32-10 draws, a log built from IEEE
-// +,-,*,/ only, and an fp64 misfit summed in observation order.
+// The per-chain step pieces live in mcmc_device.h (shared with the chain
+// epilogue of the multi-step FSM launch).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "mcmc_common.h"
+#include "mcmc_device.h"
 
 namespace {
 
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
-{
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-        uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
-        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-        c[1] = (uint32_t)p1; c[3] = (uint32_t)p0; c[0] = n0; c[2] = n2;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-}
 
-// Natural log from IEEE basic operations only (host twin: oracle_det_log).
-__device__ __forceinline__ double det_log(double x)
-{
-    uint64_t b = __double_as_longlong(x);
-    int e = (int)((b >> 52) & 0x7ff) - 1023;
-    double m = __longlong_as_double((long long)((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
-    if (m > 1.4142135623730951) { m = m * 0.5; e = e + 1; }
-    double s = (m - 1.0) / (m + 1.0), s2 = s * s;
-    double p = 1.0 / 25.0;
-    p = p * s2 + 1.0 / 23.0; p = p * s2 + 1.0 / 21.0; p = p * s2 + 1.0 / 19.0;
-    p = p * s2 + 1.0 / 17.0; p = p * s2 + 1.0 / 15.0; p = p * s2 + 1.0 / 13.0;
-    p = p * s2 + 1.0 / 11.0; p = p * s2 + 1.0 / 9.0;  p = p * s2 + 1.0 / 7.0;
-    p = p * s2 + 1.0 / 5.0;  p = p * s2 + 1.0 / 3.0;  p = p * s2 + 1.0;
-    double de = (double)e;
-    return de * 6.93147180369123816490e-01 + (2.0 * s * p + de * 1.90821492927058770002e-10);
-}
-
-// One proposal per chain: a single inversion cell of one of the chain's
-// nphase models moves by +-[1, dvmax] m/s (cell drawn over [0, nphase*ncell):
-// with one model exactly the P-only draw).  slow_prop (== slow_cur everywhere
-// but the proposed cell) gets the new cell.
+// One proposal per chain (mcmc_device.h chain_propose).
 __global__ void propose_kernel(McmcDev D, uint64_t step)
 {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= D.nchains) return;
-    uint32_t ctr[4] = {(uint32_t)step, (uint32_t)(step >> 32), 0u, 0u};
-    philox4x32_10(ctr, (uint32_t)(D.chain_offset + c), D.seed);
-    int cell = (int)(((uint64_t)ctr[0] * (uint32_t)D.ncm) >> 32);
-    int mag = 1 + (int)(((uint64_t)ctr[1] * (uint32_t)D.dvmax) >> 32);
-    const int ph = cell >= D.ncell ? 1 : 0;
-    int vold = D.v[(size_t)c * D.ncm + cell];
-    int vn = vold + ((ctr[2] & 1u) ? -mag : mag);
-    int inp = ph ? (vn >= D.vsmin && vn <= D.vsmax) : (vn >= D.vmin && vn <= D.vmax);
-    D.prop_cell[c] = cell;
-    D.prop_phase[c] = ph;
-    D.prop_v[c] = vn;
-    D.prop_inprior[c] = inp;
-    D.prop_logu[c] = det_log(((double)ctr[3] + 0.5) * (1.0 / 4294967296.0));
-    if (inp) D.slow_prop[(size_t)c * D.ncm + cell] = 1.0f / (float)vn;
-}
-
-// logL = -sum_e objfn_e, objfn_e the L2 misfit with analytic origin time
-// (locate.c:923-1047 at one grid point, iwantOT = 1), observations in CSR
-// order; an S observation is fit against the S model's table of its station
-// (the locator stacks both phases, locate.f90:399,442).  Tables of phase pph
-// come from the proposal's tables, the others from the current ones (pph < 0:
-// every phase from ttab_cur; nphase 1 uses pph = 0).
-__device__ double chain_loglik(const McmcDev &D, int c, int pph)
-{
-    const float *tp = D.ttab + (size_t)c * D.nstat * D.nev;
-    const float *tcur = D.ttab_cur ? D.ttab_cur + (size_t)c * D.nphase * D.nstat * D.nev : nullptr;
-    const double sqrt2i = 0.7071067811865475;
-    double logl = 0.0;
-    auto te_of = [&](int j, int e) -> double {
-        const int ph = D.obs_phase ? D.obs_phase[j] : 0;
-        const size_t k = (size_t)D.obs_stat[j] * D.nev + e;
-        return (double)(ph == pph ? tp[k] : tcur[(size_t)ph * D.nstat * D.nev + k]);
-    };
-    for (int e = 0; e < D.nev; e++) {
-        int j0 = D.obs_ptr[e], j1 = D.obs_ptr[e + 1];
-        double xnorm = 0.0, t0 = 0.0, obj = 0.0;
-        for (int j = j0; j < j1; j++) if (!D.obs_mask[j]) xnorm = xnorm + 1.0 / D.var[j];
-        for (int j = j0; j < j1; j++) {
-            if (D.obs_mask[j]) continue;
-            double te = te_of(j, e);
-            double tc = D.tobs[j] - D.tcorr[j];
-            t0 = t0 + ((1.0 / D.var[j]) / xnorm) * (tc - te);
-        }
-        for (int j = j0; j < j1; j++) {
-            if (D.obs_mask[j]) continue;
-            double te = te_of(j, e);
-            double tc = D.tobs[j] - D.tcorr[j];
-            double res = ((1.0 / D.var[j]) * sqrt2i) * (tc - (te + t0));
-            obj = obj + res * res;
-        }
-        logl = logl - obj;
-    }
-    return logl;
+    mcmcd::chain_propose(D, c, step);
 }
 
 __global__ void init_loglik_kernel(McmcDev D)
 {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= D.nchains) return;
-    D.logl[c] = chain_loglik(D, c, D.nphase > 1 ? -1 : 0);
+    D.logl[c] = mcmcd::chain_loglik(D, c, D.nphase > 1 ? -1 : 0);
 }
 
-// Metropolis accept/reject; keeps slow_cur/slow_prop identical except while a
-// proposal is pending, so each step touches one cell per chain.  With two
-// models an accepted proposal's tables become its phase's current tables.
+// Metropolis accept/reject (mcmc_device.h chain_accept); with two models an
+// accepted proposal's tables become its phase's current tables.
 __global__ void accept_kernel(McmcDev D, int keep_slot)
 {
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= D.nchains) return;
-    int cell = D.prop_cell[c];
-    size_t ci = (size_t)c * D.ncm + cell;
-    int acc = 0;
-    if (D.prop_inprior[c]) {
-        const int ph = D.prop_phase[c];
-        double ln = chain_loglik(D, c, ph);
-        acc = D.prop_logu[c] < ln - D.logl[c];
-        if (acc) {
-            D.logl[c] = ln;
-            D.v[ci] = D.prop_v[c];
-            D.slow_cur[ci] = D.slow_prop[ci];
-            D.naccept[c] += 1;
-            if (D.nphase > 1) {
-                const size_t n = (size_t)D.nstat * D.nev;
-                const float *src = D.ttab + (size_t)c * n;
-                float *dst = D.ttab_cur + ((size_t)c * D.nphase + ph) * n;
-                for (size_t k = 0; k < n; k++) dst[k] = src[k];
-            }
-        } else {
-            D.slow_prop[ci] = D.slow_cur[ci];
-        }
-    }
-    D.accept[c] = (unsigned char)acc;
-    if (keep_slot >= 0) D.keep_logl[(size_t)keep_slot * D.keep_stride + c] = D.logl[c];
+    const int inp = D.prop_inprior[c], ph = D.prop_phase[c];
+    const double ln = inp ? mcmcd::chain_loglik(D, c, ph) : 0.0;
+    if (mcmcd::chain_accept(D, c, ln, keep_slot) && D.nphase > 1) mcmcd::chain_copy_tables(D, c, ph, 0, 1);
 }
 
 // Kept state copy: [slot][chain][nphase][ncell] int (after accept_kernel).

@@ -363,7 +363,7 @@ class Sampler:
         return {"npipe": n, "nphase": i.nphase, "step_z": i.step_z, "fixed_layout": bool(i.fixed_layout),
                 "chains": list(i.chains[:n]), "waves": list(i.waves[:n]),
                 "workspace_bytes": list(i.workspace_bytes[:n]), "lds_bytes": int(i.lds_bytes),
-                "masked_s": i.masked_s, "kernel": i.kernel.decode()}
+                "masked_s": i.masked_s, "kernel": i.kernel.decode(), "multi_step": bool(i.multi_step)}
 
     def state(self):
         v = np.empty(self.model_shape, np.int32)

@@ -72,18 +72,20 @@ def test_ps_init_tables_and_loglik_bitwise():
         assert logl0[c] == O.loglik(P, to)
 
 
-@pytest.mark.parametrize("pipes", ["1", "2"])
-def test_ps_mcmc_steps_bitwise(pipes, monkeypatch):
+@pytest.mark.parametrize("mode", ["multi", "pipes1", "pipes2"])
+def test_ps_mcmc_steps_bitwise(mode, monkeypatch):
     """8 steps of 4 chains: accept sequence, logL trace and both models ==
     oracle_mcmc_run (which re-solves both models every proposal); proposals
-    hit both models; one pipe and two pipes alike."""
+    hit both models; multi-step launches, one pipe and two pipes alike."""
     _dev()
-    monkeypatch.setenv("MCEIK_PIPES", pipes)
+    monkeypatch.setenv("MCEIK_PERSIST", "1" if mode == "multi" else "0")
+    monkeypatch.setenv("MCEIK_PIPES", "2" if mode == "pipes2" else "1")
     from mceik_amd import mcmc
     p = _ps_problem()
     nch, off, nsteps = 4, 3, 8
     s = mcmc.Sampler(p, nchains=nch, chain_offset=off)
-    assert s.info()["npipe"] == int(pipes)
+    assert s.info()["npipe"] == (2 if mode == "pipes2" else 1)
+    assert s.info()["multi_step"] == (mode == "multi")
     v0, logl0, _, _ = s.state()
     acc, trace, phases = [], [], []
     for _ in range(nsteps):
