@@ -125,7 +125,7 @@ def cpu_baseline(p, v0, cores, rounds=CPU_ROUNDS):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--chains", type=int, default=0, help="chains per GPU (default: the config's)")
