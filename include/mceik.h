@@ -64,9 +64,10 @@ typedef struct mceik_mcmc_info {
     size_t lds_bytes;          /* LDS per FSM wave                                           */
     int masked_s;              /* S observations ignored (nphase 1 with mask_s = 1)          */
     char kernel[64];           /* the FSM kernel instance (rocprof name)                    */
-    int multi_step;            /* 1 (MCEIK_PERSIST=1): one FSM launch runs up to 64 steps, no
-                                  barrier between them (the chain epilogue in the kernel);
-                                  0: per-step propose / FSM / accept launches (the default)   */
+    int multi_step;            /* 1: one FSM launch runs up to 64 steps, no barrier between
+                                  them (the chain epilogue in the kernel; default when a step
+                                  is <= 4 solves per wave, MCEIK_PERSIST=1/0 forces);
+                                  0: per-step propose / FSM / accept launches               */
 } mceik_mcmc_info;
 
 /* ---- run configuration (host only; csrc/parms.c) ----------------------

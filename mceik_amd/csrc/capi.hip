@@ -1580,10 +1580,14 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     s->report = report;
     if (report) clock_report(s, "init");
     s->npipe = 1;
-    // MCEIK_PERSIST=1: multi-step launches where eligible (measured slower than
-    // two pipes at C3, DESIGN.md s.3.5, so off by default)
+    // Multi-step launches by default where a step is at most
+    // 4 solves per resident wave (the per-step tail is then a large share: C2
+    // +1.1% over two pipes; at C3's 16 solves per wave two pipes are 1% ahead);
+    // MCEIK_PERSIST=1 / 0 forces them on / off
     const char *persist_env = getenv("MCEIK_PERSIST");
-    s->persist = persist_env && persist_env[0] == '1' && b.precision == 32 && mceik_fsm_step_z(&b) == 16 && !lpt;
+    const bool short_steps = (long long)b.nmodel * b.nstat <= 4LL * ws_layout(&b).nwaves;
+    s->persist = (persist_env ? persist_env[0] == '1' : short_steps) && b.precision == 32 &&
+                 mceik_fsm_step_z(&b) == 16 && !lpt;
     if (s->persist && (dalloc(s, &s->d_sync, MC_SYNC_WORDS(nch)) || dput(s, &s->d_dev, &D, 1))) {
         mceik_mcmc_finalize(&s);
         return -1;

@@ -221,18 +221,25 @@ def test_station_on_first_node_fails_init():
 
 
 
-@pytest.mark.parametrize("nch,pipes", [(5, "2"), (8, "2"), (5, "1"), (7, "3")], ids=["odd_halves", "even_halves", "one_pipe", "three_pipes"])
+@pytest.mark.parametrize("nch,pipes", [(5, "2"), (8, "2"), (5, "1"), (7, "3"), (5, "multi"), (9, "multi")],
+                         ids=["odd_halves", "even_halves", "one_pipe", "three_pipes", "multi_step", "multi_step_9"])
 def test_pipes_bitwise(nch, pipes, monkeypatch):
-    """Two pipes (the default: halves of the chains on two streams, DESIGN.md
-    s.3.5) and one pipe (MCEIK_PIPES=1): models, logL, accept counts and kept
-    samples bit-identical to oracle_mcmc_run, with run() split over calls."""
+    """Two pipes (halves of the chains on two streams), one
+    pipe (MCEIK_PIPES=1), three, and multi-step launches (MCEIK_PERSIST=1: the
+    accept, kept state and next proposal inside the FSM kernel): models, logL,
+    accept counts and kept samples bit-identical to oracle_mcmc_run, with
+    run() split over calls (kept-state slots carried across launches)."""
     _dev()
     from mceik_amd import mcmc
-    monkeypatch.setenv("MCEIK_PIPES", pipes)
-    p = _problem(n=40, seed=9)
+    monkeypatch.setenv("MCEIK_PERSIST", "1" if pipes == "multi" else "0")
+    monkeypatch.setenv("MCEIK_PIPES", "1" if pipes == "multi" else pipes)
+    p = _problem(n=64 if pipes == "multi" else 40, seed=9)     # (64^3: the 16-z kernel, which runs multi-step)
     p.nburn, p.keepk = 1, 2                   # kept after steps 2, 4, 6
     off = 3
     s = mcmc.Sampler(p, nchains=nch, chain_offset=off, max_samples=8)
+    info = s.info()
+    assert info["multi_step"] == (pipes == "multi")
+    assert info["npipe"] == (1 if pipes == "multi" else int(pipes))
     v0, logl0, _, _ = s.state()
     s.run(2)
     s.run(1)
