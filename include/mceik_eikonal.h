@@ -38,15 +38,21 @@ void eikonal3d_serial_driver_sp(const int *job, const int *iverb, const int *max
 
 /* Replaces the MPI variant EIKONAL3D_INITIALIZE / _SOLVE / _FINALIZE
  * (fsm3d.f90:1583-1598, 1754-1769, 1891-1899), every argument by pointer.
- * One GPU holds the whole grid (comm is not used) but the decomposition is
+ * Collective over comm (MPI resolved at run time; no MPI = one rank): rank
+ * 0's parameters and SETBCS error reach every rank.  The decomposition is
  * honoured: ndivx x ndivy x ndivz blocks (noverlap: ghost layer width, 0 =
  * block faces act as grid edges) run the reference's block-decomposed FSM
  * (EIKONAL3D_FSM_MPI: each block sweeps its nodes against ghost copies
  * refreshed after every sweep), so u and ierr are bitwise the reference's run
- * with one MPI rank per block; one block = the serial driver's solve.  The
- * master passes the full arrays (n = nx*ny*nz) and receives u; a rank passing
- * n < nx*ny*nz (the reference's callers use n = 1) returns at once with
- * ierr = 0.  fp64 (xfsm3d: max u = 1.4308203212738235). */
+ * with one MPI rank per block; one block = the serial driver's solve.  With
+ * as many ranks in comm as blocks (the reference's layout) every rank sweeps
+ * its own block on its GPU and swaps face layers with its neighbours after
+ * every sweep (RCCL when each rank has a GPU of its own, host-staged MPI when
+ * ranks share one; MCEIK_HALO=mpi|rccl), and the master gathers u; otherwise
+ * the master's GPU runs every block.  The master passes the full arrays
+ * (n = nx*ny*nz) and receives u; the other ranks pass n = 1 as the
+ * reference's callers do and keep their u.  fp64 (xfsm3d: max u =
+ * 1.4308203212738235). */
 void eikonal3d_initialize(const int *comm, const int *iverb, const int *nx, const int *ny, const int *nz,
                           const int *ndivx, const int *ndivy, const int *ndivz, const int *noverlap,
                           const int *maxit, const double *x0, const double *y0, const double *z0,

@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <vector>
@@ -18,6 +19,7 @@
 #include "fsm_common.h"
 #include "mcmc_common.h"
 #include "fsm_single.h"
+#include "rccl_rt.h"
 
 hipError_t fsm_launch(const FsmLaunch &L, int is_double, int nwaves, hipStream_t st);
 hipError_t fsm_zero_words(unsigned *p, int n, hipStream_t st);
@@ -692,7 +694,7 @@ static int blocks_solve(SingleState &S, int nsrc, const double *ts, const double
                 return -1;
         unsigned count = 0;
         if (hipMemsetAsync(S.d_count, 0, 4, st) != hipSuccess ||
-            fsm_block_unconverged(L, S.tol, S.d_count, st) != hipSuccess ||
+            fsm_block_unconverged(L, BlockBox{{0, 0, 0}, {L.nx, L.ny, L.nz}}, S.tol, S.d_count, st) != hipSuccess ||
             hipMemcpyAsync(&count, S.d_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipMemcpyAsync(&ierr, d_ierr, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
@@ -710,17 +712,322 @@ static int blocks_solve(SingleState &S, int nsrc, const double *ts, const double
 // MPI of the calling process, resolved at run time (csrc/mpi_rt.c): -1 = the
 // caller runs no MPI (a single process: rank 0 of one).
 extern "C" int mceik_mpi_rank(int fcomm);
+extern "C" int mceik_mpi_size(int fcomm);
 extern "C" int mceik_mpi_bcast_int(int fcomm, int *v, int n, int root);
 extern "C" int mceik_mpi_bcast_double(int fcomm, double *v, int n, int root);
+extern "C" int mceik_mpi_allreduce_int(int fcomm, int *v, int n, int op);
+extern "C" int mceik_mpi_allgather_bytes(int fcomm, const void *mine, void *all, int nbytes);
+extern "C" int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, const int *peer, const int *tag,
+                                         double *const *buf, const int *count);
+
+// ---- the MPI variant across ranks: one block per rank -----------------------
+// With as many ranks in comm as blocks (the reference's own layout,
+// fsm3d.f90:1069-1074: rank r owns block r, x fastest, MPIUTILS_GRD2IJK), the
+// solve is distributed as the reference's EIKONAL3D_FSM_MPI: every rank sweeps
+// the block it owns on its own GPU, swaps the one-node face layers with the
+// ranks owning the adjacent blocks after every sweep (EIKONAL_EXCHANGE,
+// :971-1046; only the first ghost layer is ever read), sums the unconverged
+// nodes over ranks after every iteration (:198-211) and sends its block to the
+// master at the end (EIKONAL_GATHER_TRAVELTIMES).  Each rank keeps the grid in
+// the padded global layout (nodes outside its block and its faces stay at their
+// SETBCS values; a 512^3 fp64 field is 1 GiB of the 288 GB), so the sweep is
+// the one-GPU block kernel restricted to block b0 with the ghost snapshot
+// being u itself.  Transport of the face layers: RCCL device to device when
+// every rank has a GPU of its own (xGMI), host-staged MPI when ranks share a
+// GPU (RCCL takes one rank per GPU); MCEIK_HALO=mpi|rccl overrides.
+struct RankHalo {
+    int on;                      // the solve runs one block per rank
+    int fcomm, rank, nranks;
+    BlockBox own;                // the block this rank owns (= its rank)
+    int kind;                    // 1: host-staged MPI, 2: RCCL
+    int peer[6], tag_send[6], tag_recv[6];
+    BoxList send, recv;          // faces sent / received, in the same face order
+    double *d_buf;               // device: send faces, then receive faces
+    double *h_buf;               // pinned host staging (MPI transport)
+    ncclComm_t nc;
+};
+static RankHalo g_halo;
+
+// Block b of the decomposition (fsm3d.f90:1086-1098; ext may be <= 0 when
+// there are more blocks than nodes, which the reference rejects).
+static void decomp_block(const BlockDecomp &D, const int nn[3], int b, int lo[3], int ext[3])
+{
+    const int bi[3] = {b % D.nd[0], (b / D.nd[0]) % D.nd[1], b / (D.nd[0] * D.nd[1])};
+    for (int a = 0; a < 3; a++) {
+        lo[a] = D.step[a] * bi[a];
+        const int hi = bi[a] + 1 == D.nd[a] ? nn[a] - 1 : D.step[a] * (bi[a] + 1) - 1;
+        ext[a] = hi - lo[a] + 1;
+    }
+}
+
+// The reference's check that the blocks tile the grid (fsm3d.f90:1105-1112).
+static bool decomp_tiles(const BlockDecomp &D, const int nn[3])
+{
+    long long tot = 0;
+    for (int b = 0; b < D.nd[0] * D.nd[1] * D.nd[2]; b++) {
+        int lo[3], ext[3];
+        decomp_block(D, nn, b, lo, ext);
+        tot += (long long)ext[0] * ext[1] * ext[2];
+    }
+    return tot == (long long)nn[0] * nn[1] * nn[2];
+}
+
+static void halo_free(RankHalo &H)
+{
+    if (H.nc) mceik_rccl().CommDestroy(H.nc);
+    if (H.d_buf) hipFree(H.d_buf);
+    if (H.h_buf) hipHostFree(H.h_buf);
+    memset(&H, 0, sizeof(H));
+}
+
+// Face plan, buffers and transport of this rank (collective over comm).
+// Returns 0, or 1 when any rank failed (every rank returns alike).
+static int halo_setup(RankHalo &H, const BlockDecomp &D, const int nn[3], int fcomm, int rank, int nranks)
+{
+    halo_free(H);
+    H.fcomm = fcomm; H.rank = rank; H.nranks = nranks;
+    int lo[3], ext[3];
+    decomp_block(D, nn, rank, lo, ext);
+    for (int a = 0; a < 3; a++) { H.own.lo[a] = lo[a]; H.own.ext[a] = ext[a]; }
+    const int bi[3] = {rank % D.nd[0], (rank / D.nd[0]) % D.nd[1], rank / (D.nd[0] * D.nd[1])};
+    int nf = 0;
+    H.send.off[0] = H.recv.off[0] = 0;
+    const bool empty = ext[0] <= 0 || ext[1] <= 0 || ext[2] <= 0;
+    for (int a = 0; a < 3 && D.nov > 0 && !empty; a++)
+        for (int s = 0; s < 2; s++) {
+            const int nb = bi[a] + (s ? 1 : -1);
+            if (nb < 0 || nb >= D.nd[a]) continue;
+            int nbi[3] = {bi[0], bi[1], bi[2]};
+            nbi[a] = nb;
+            int nlo[3], next[3];
+            decomp_block(D, nn, nbi[0] + D.nd[0] * (nbi[1] + D.nd[1] * nbi[2]), nlo, next);
+            if (next[0] <= 0 || next[1] <= 0 || next[2] <= 0) continue;      // an empty neighbour sends nothing
+            BlockBox sb = H.own, rb = H.own;
+            sb.ext[a] = rb.ext[a] = 1;
+            sb.lo[a] = s ? lo[a] + ext[a] - 1 : lo[a];
+            rb.lo[a] = s ? lo[a] + ext[a] : lo[a] - 1;
+            H.peer[nf] = nbi[0] + D.nd[0] * (nbi[1] + D.nd[1] * nbi[2]);
+            H.tag_send[nf] = 2 * a + s;
+            H.tag_recv[nf] = 2 * a + 1 - s;
+            H.send.box[nf] = sb;
+            H.recv.box[nf] = rb;
+            const size_t cnt = (size_t)sb.ext[0] * sb.ext[1] * sb.ext[2];
+            H.send.off[nf + 1] = H.send.off[nf] + cnt;
+            H.recv.off[nf + 1] = H.recv.off[nf] + cnt;
+            nf++;
+        }
+    H.send.n = H.recv.n = nf;
+    const size_t nsend = H.send.off[nf], nrecv = H.recv.off[nf];
+    int e = 0;
+    if (nsend + nrecv > 0 &&
+        (hipMalloc(&H.d_buf, (nsend + nrecv) * 8) != hipSuccess ||
+         hipHostMalloc(&H.h_buf, (nsend + nrecv) * 8, hipHostMallocDefault) != hipSuccess))
+        e = 1;
+    // transport: RCCL only when no two ranks share a GPU
+    const char *env = getenv("MCEIK_HALO");
+    int want = env && !strcmp(env, "mpi") ? 1 : env && !strcmp(env, "rccl") ? 2 : 0;
+    if (!want) {
+        char id[128] = {0};
+        int dev = 0;
+        gethostname(id, 64);
+        id[63] = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(id + 64, 64, dev) != hipSuccess) e = 1;
+        std::vector<char> all((size_t)nranks * 128);
+        want = 2;
+        if (mceik_mpi_allgather_bytes(fcomm, id, all.data(), 128)) e = 1;
+        for (int r = 0; r < nranks && want == 2; r++)
+            for (int q = 0; q < r; q++)
+                if (!memcmp(&all[(size_t)r * 128], &all[(size_t)q * 128], 128)) { want = 1; break; }
+    }
+    if (mceik_mpi_allreduce_int(fcomm, &e, 1, 1)) e = 1;
+    if (!e && want == 2) {
+        int idw[MCEIK_COMM_ID_BYTES / 4] = {0};
+        int ie = !mceik_rccl().ok;
+        if (mceik_mpi_allreduce_int(fcomm, &ie, 1, 1) || ie) e = 1;
+        ncclUniqueId uid;
+        if (!e && rank == 0) {
+            ie = mceik_rccl().GetUniqueId(&uid) != ncclSuccess;
+            memcpy(idw, &uid, sizeof(uid));
+        }
+        if (!e && (mceik_mpi_bcast_int(fcomm, &ie, 1, 0) || ie || mceik_mpi_bcast_int(fcomm, idw, MCEIK_COMM_ID_BYTES / 4, 0)))
+            e = 1;
+        if (!e) {
+            memcpy(&uid, idw, sizeof(uid));
+            ie = mceik_rccl().CommInitRank(&H.nc, nranks, uid, rank) != ncclSuccess;
+            if (ie) H.nc = nullptr;
+            if (mceik_mpi_allreduce_int(fcomm, &ie, 1, 1) || ie) e = 1;
+        }
+    }
+    H.kind = want;
+    if (e) {
+        halo_free(H);
+        return 1;
+    }
+    H.on = 1;
+    return 0;
+}
+
+// One face swap after a sweep: pack the faces this rank owns, swap them with
+// the neighbours, unpack the ones received.  Returns nonzero on a failure
+// (a failing rank still takes part in the messages, so none is left waiting).
+static int halo_swap(RankHalo &H, const SingleLaunch &L, hipStream_t st, int fail)
+{
+    const int nf = H.send.n;
+    if (nf == 0) return fail;
+    const size_t nsend = H.send.off[nf], nrecv = H.recv.off[nf];
+    double *d_recv = H.d_buf + nsend;
+    if (H.kind == 2) {
+        if (!fail && fsm_box_copy(L, H.send, H.d_buf, 1, st) != hipSuccess) fail = 1;
+        bool ok = mceik_rccl().GroupStart() == ncclSuccess;
+        for (int f = 0; f < nf && ok; f++)
+            ok = mceik_rccl().Send(H.d_buf + H.send.off[f], H.send.off[f + 1] - H.send.off[f], ncclFloat64, H.peer[f],
+                                   H.nc, st) == ncclSuccess &&
+                 mceik_rccl().Recv(d_recv + H.recv.off[f], H.recv.off[f + 1] - H.recv.off[f], ncclFloat64, H.peer[f],
+                                   H.nc, st) == ncclSuccess;
+        ok = mceik_rccl().GroupEnd() == ncclSuccess && ok;
+        if (!ok) fail = 1;
+        if (!fail && fsm_box_copy(L, H.recv, d_recv, 0, st) != hipSuccess) fail = 1;
+        return fail;
+    }
+    if (!fail && (fsm_box_copy(L, H.send, H.d_buf, 1, st) != hipSuccess ||
+                  hipMemcpyAsync(H.h_buf, H.d_buf, nsend * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                  hipStreamSynchronize(st) != hipSuccess))
+        fail = 1;
+    int dir[12], peer[12], tag[12], cnt[12];
+    double *buf[12];
+    for (int f = 0; f < nf; f++) {
+        dir[2 * f] = 0; peer[2 * f] = H.peer[f]; tag[2 * f] = H.tag_send[f];
+        buf[2 * f] = H.h_buf + H.send.off[f]; cnt[2 * f] = (int)(H.send.off[f + 1] - H.send.off[f]);
+        dir[2 * f + 1] = 1; peer[2 * f + 1] = H.peer[f]; tag[2 * f + 1] = H.tag_recv[f];
+        buf[2 * f + 1] = H.h_buf + nsend + H.recv.off[f]; cnt[2 * f + 1] = (int)(H.recv.off[f + 1] - H.recv.off[f]);
+    }
+    if (mceik_mpi_exchange_double(H.fcomm, 2 * nf, dir, peer, tag, buf, cnt)) fail = 1;
+    if (!fail && (hipMemcpyAsync(d_recv, H.h_buf + nsend, nrecv * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                  fsm_box_copy(L, H.recv, d_recv, 0, st) != hipSuccess))
+        fail = 1;
+    return fail;
+}
+
+// The distributed solve (collective over comm; the master's slow/u are the
+// whole grid, the others' are not read or written).  Every rank returns its own
+// ierr as the reference's (SETBCS: the same on every rank; the solver: the
+// ierr of its local grid's last level), -1 on a failure on any rank.
+static int blocks_solve_ranks(SingleState &S, RankHalo &H, int nsrc, const double *ts, const double *xs,
+                              const double *ys, const double *zs, const double *slow, double *u)
+{
+    SingleLaunch &L = S.L;
+    const size_t n = (size_t)L.nx * L.ny * L.nz, np = (size_t)L.nxp * L.nyp * L.nzp;
+    L.maxit = S.maxit; L.tol = S.tol; L.h = S.h; L.x0 = S.x0; L.y0 = S.y0; L.z0 = S.z0;
+    const bool master = H.rank == 0;
+    // the master's model and sources on every rank (EIKONAL_SCATTER_MODEL's role)
+    std::vector<double> src((size_t)nsrc * 4), mslow(master ? 0 : n);
+    if (master)
+        for (int k = 0; k < nsrc; k++) {
+            src[k * 4 + 0] = ts[k]; src[k * 4 + 1] = xs[k]; src[k * 4 + 2] = ys[k]; src[k * 4 + 3] = zs[k];
+        }
+    const double *sl = master ? slow : mslow.data();
+    if (mceik_mpi_bcast_double(H.fcomm, src.data(), nsrc * 4, 0) ||
+        mceik_mpi_bcast_double(H.fcomm, (double *)sl, (int)n, 0))
+        return -1;
+    hipStream_t st = S.st;
+    const BlockBox own = H.own;
+    const bool empty = own.ext[0] <= 0 || own.ext[1] <= 0 || own.ext[2] <= 0;
+    int fail = 0, ierr_bc = 0, ierr = 0;
+    if (hipMemcpyAsync(S.dense, sl, n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(S.src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        fsm_single_pad(S.dense, (void *)L.slow, 1, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
+        fsm_single_setbcs(L, S.src, nsrc, S.ierr_bc, st) != hipSuccess ||
+        hipMemcpyAsync(&ierr_bc, S.ierr_bc, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        fail = 1;
+    int agree[2] = {fail, ierr_bc};                  // SETBCS runs alike everywhere; the master's error counts
+    if (mceik_mpi_allreduce_int(H.fcomm, agree, 2, 1)) return -1;
+    if (agree[0]) return -1;
+    S.bcfail = agree[1] != 0;
+    if (S.bcfail) return 1;
+    int *d_ierr = (int *)(S.d_count + 1);
+    for (int k = 1; k <= S.maxit; k++) {
+        if (!fail && hipMemcpyAsync(L.u0, L.u, np * 8, hipMemcpyDeviceToDevice, st) != hipSuccess) fail = 1;
+        for (int g = 0; g < 8; g++) {
+            if (!fail && (hipMemsetAsync(d_ierr, 0, 4, st) != hipSuccess ||
+                          fsm_block_sweep(L, S.D, (const double *)L.u, g, d_ierr, st, H.rank, empty ? 0 : 1,
+                                          H.rank) != hipSuccess))
+                fail = 1;
+            fail = halo_swap(H, L, st, fail);
+        }
+        unsigned count = 0;
+        if (!fail && (hipMemsetAsync(S.d_count, 0, 4, st) != hipSuccess ||
+                      (!empty && fsm_block_unconverged(L, own, S.tol, S.d_count, st) != hipSuccess) ||
+                      hipMemcpyAsync(&count, S.d_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                      hipMemcpyAsync(&ierr, d_ierr, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                      hipStreamSynchronize(st) != hipSuccess))
+            fail = 1;
+        int tot[2] = {(int)std::min<unsigned>(count, 1u << 30), fail};
+        if (mceik_mpi_allreduce_int(H.fcomm, tot, 2, 0)) return -1;
+        if (tot[1]) return -1;
+        if (tot[0] == 0) break;
+    }
+    // every block to the master
+    BoxList mine;
+    mine.n = 1; mine.box[0] = own; mine.off[0] = 0;
+    mine.off[1] = empty ? 0 : (size_t)own.ext[0] * own.ext[1] * own.ext[2];
+    if (master) {
+        std::vector<std::vector<double>> got(H.nranks);
+        std::vector<int> dir, peer, tag, cnt;
+        std::vector<double *> buf;
+        std::vector<BlockBox> box(H.nranks);
+        const int nn[3] = {L.nx, L.ny, L.nz};
+        for (int r = 1; r < H.nranks; r++) {
+            int lo[3], ext[3];
+            decomp_block(S.D, nn, r, lo, ext);
+            for (int a = 0; a < 3; a++) { box[r].lo[a] = lo[a]; box[r].ext[a] = ext[a] > 0 ? ext[a] : 0; }
+            const size_t c = (size_t)box[r].ext[0] * box[r].ext[1] * box[r].ext[2];
+            if (!c) continue;
+            got[r].resize(c);
+            dir.push_back(1); peer.push_back(r); tag.push_back(99); cnt.push_back((int)c); buf.push_back(got[r].data());
+        }
+        if (!fail && (fsm_single_unpad(L.u, S.dense, 1, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
+                      hipMemcpyAsync(u, S.dense, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                      hipStreamSynchronize(st) != hipSuccess))
+            fail = 1;
+        if (mceik_mpi_exchange_double(H.fcomm, (int)dir.size(), dir.data(), peer.data(), tag.data(), buf.data(),
+                                      cnt.data()))
+            fail = 1;
+        for (int r = 1; r < H.nranks && !fail; r++) {
+            const BlockBox &B = box[r];
+            size_t i = 0;
+            for (int z = 0; z < B.ext[2]; z++)
+                for (int y = 0; y < B.ext[1]; y++) {
+                    memcpy(u + ((size_t)(B.lo[2] + z) * L.ny + B.lo[1] + y) * L.nx + B.lo[0], &got[r][i],
+                           (size_t)B.ext[0] * 8);
+                    i += B.ext[0];
+                }
+        }
+    } else if (mine.off[1]) {
+        std::vector<double> out(mine.off[1]);
+        if (fsm_box_copy(L, mine, S.dense, 1, st) != hipSuccess ||
+            hipMemcpyAsync(out.data(), S.dense, out.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            fail = 1;
+        int dir = 0, peer = 0, tag = 99, cnt = (int)out.size();
+        double *b = out.data();
+        if (mceik_mpi_exchange_double(H.fcomm, 1, &dir, &peer, &tag, &b, &cnt)) fail = 1;
+    }
+    if (mceik_mpi_allreduce_int(H.fcomm, &fail, 1, 1) || fail) return -1;
+    return ierr;
+}
 
 // The MPI variant is collective over comm as the reference's
 // (fsm3d.f90:1583-1929): the master (rank 0) broadcasts its parameters at
 // initialize (:1626-1639) and its error at solve (:1792) and every rank
-// returns it.  One GPU holds the whole grid, so the master alone solves; the
-// other ranks take part in the broadcasts and keep their u untouched.  A
-// process without MPI is the master of one rank, except that a call passing
-// n < nx*ny*nz to solve acts as a non-master rank (the reference's callers
-// pass n = 1 there, fsm3d.f90:2102-2106) and returns ierr = 0.
+// returns it.  With as many ranks as blocks the solve is distributed, one
+// block per rank (RankHalo above).  Otherwise one GPU holds the whole grid and
+// the master alone solves (every block, when there are several, by the
+// one-GPU block iteration); the other ranks take part in the broadcasts and
+// keep their u untouched.  A process without MPI is the master of one rank,
+// except that a call passing n < nx*ny*nz to solve acts as a non-master rank
+// (the reference's callers pass n = 1 there, fsm3d.f90:2102-2106) and returns
+// ierr = 0.
 static int mpi_variant_rank(const int *comm) { return comm ? mceik_mpi_rank(*comm) : -1; }
 
 extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const int *nx, const int *ny, const int *nz,
@@ -731,6 +1038,7 @@ extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const in
     SingleState &S = g_single[2];
     *ierr = 0;
     const int rank = mpi_variant_rank(comm);
+    const int nranks = rank >= 0 ? mceik_mpi_size(*comm) : 1;
     // the master's parameters on every rank
     int ip[9] = {*iverb, *nx, *ny, *nz, *ndivx, *ndivy, *ndivz, *noverlap, *maxit};
     double dp[5] = {*x0, *y0, *z0, *h, *tol};
@@ -741,23 +1049,34 @@ extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const in
     }
     if (ip[0] > 0 && rank <= 0) printf(" eikonal3d_initialize: Broadcasting parameters...\n");
     int e = 0;
-    if (ip[4] < 1 || ip[5] < 1 || ip[6] < 1 || ip[7] < 0) {
-        if (rank <= 0) printf(" eikonal3d_initialize: Error computing local domain\n");
+    const int nd[3] = {ip[4], ip[5], ip[6]}, nn[3] = {ip[1], ip[2], ip[3]};
+    BlockDecomp D{};
+    if (ip[4] < 1 || ip[5] < 1 || ip[6] < 1 || ip[7] < 0 || nn[0] < 1 || nn[1] < 1 || nn[2] < 1) {
+        e = 1;
+    } else {
+        for (int a = 0; a < 3; a++) {
+            D.nd[a] = nd[a];
+            D.step[a] = nn[a] / nd[a] > 1 ? nn[a] / nd[a] : 1;       // fsm3d.f90:1086-1088
+        }
+        D.nov = ip[7];
+        if (!decomp_tiles(D, nn)) e = 1;
+    }
+    if (e && rank <= 0) printf(" eikonal3d_initialize: Error computing local domain\n");
+    const bool ranks = !e && rank >= 0 && nranks > 1 && nranks == nd[0] * nd[1] * nd[2];
+    halo_free(g_halo);
+    if (!e && (rank <= 0 || ranks)) {            // the grid on the master's GPU, or on every rank's
+        if (single_alloc(S, 1, nn[0], nn[1], nn[2], ip[8], 1)) e = 2;
+        S.D = D;
+        if (!e && (nd[0] * nd[1] * nd[2] > 1) && blocks_buffers(S)) e = 2;
+        if (e == 2) printf(" eikonal3d_initialize: Error making the device structures on process %d\n",
+                           rank > 0 ? rank : 0);
+    }
+    // a failure on any rank's device is every rank's failure
+    if (rank >= 0 && mceik_mpi_allreduce_int(*comm, &e, 1, 1)) e = 1;
+    if (!e && ranks && halo_setup(g_halo, D, nn, *comm, rank, nranks)) {
+        if (rank == 0) printf(" eikonal3d_initialize: Error making the ghost communication structure\n");
         e = 1;
     }
-    const int nd[3] = {ip[4], ip[5], ip[6]}, nn[3] = {ip[1], ip[2], ip[3]};
-    if (!e && rank <= 0) {            // the grid lives on the master's GPU
-        if (single_alloc(S, 1, nn[0], nn[1], nn[2], ip[8], 1)) e = 2;
-        for (int a = 0; a < 3 && !e; a++) {
-            S.D.nd[a] = nd[a];
-            S.D.step[a] = nn[a] / nd[a] > 1 ? nn[a] / nd[a] : 1;       // fsm3d.f90:1086-1088
-        }
-        S.D.nov = ip[7];
-        if (!e && nd[0] * nd[1] * nd[2] > 1 && blocks_buffers(S)) e = 2;
-        if (e == 2) printf(" eikonal3d_initialize: Error making the device structures\n");
-    }
-    // a failure on the master's device is every rank's failure
-    if (rank >= 0 && mceik_mpi_bcast_int(*comm, &e, 1, 0)) e = 1;
     if (e) {
         *ierr = 1;
         return;
@@ -780,6 +1099,28 @@ extern "C" void eikonal3d_solve(const int *comm, const int *nsrc, const int *n, 
     }
     int e = 0;
     const bool master = rank == 0 || (rank < 0 && (long)*n >= (long)S.nx * S.ny * S.nz);
+    if (g_halo.on) {
+        // the master's source count and argument check on every rank
+        int mp[2] = {*nsrc, 0};
+        if (master && (*nsrc < 1 || (long)*n < (long)S.nx * S.ny * S.nz)) mp[1] = 1;
+        if (mceik_mpi_bcast_int(*comm, mp, 2, 0)) mp[1] = 1;
+        if (!mp[1] && single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, mp[0])) mp[1] = 2;
+        if (mceik_mpi_allreduce_int(*comm, &mp[1], 1, 1)) mp[1] = 1;
+        if (mp[1]) {
+            if (master) printf(" eikonal3d_solve: Error setting bcs\n");
+            *ierr = 1;
+            return;
+        }
+        if (master && S.iverb > 0) printf(" eikonal3d_solve: Setting boundary conditions...\n");
+        const int rc = blocks_solve_ranks(S, g_halo, mp[0], ts, xs, ys, zs, slow, u);
+        if (S.bcfail) {
+            if (master) printf(" eikonal3d_solve: Error setting bcs\n");
+        } else if (rc != 0) {
+            printf(" eikonal3d_solve: Error calling solver on process %d\n", rank);
+        }
+        *ierr = rc < 0 ? 1 : rc;
+        return;
+    }
     if (master) {
         const bool blocks = S.D.nd[0] * S.D.nd[1] * S.D.nd[2] > 1;
         if (*nsrc < 1 || (long)*n < (long)S.nx * S.ny * S.nz || single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, *nsrc) ||
@@ -810,6 +1151,7 @@ extern "C" void eikonal3d_finalize(const int *comm, int *ierr)
         *ierr = 1;
     }
     if (mpi_variant_rank(comm) <= 0 && S.iverb > 0) printf(" eikonal3d_finalize: Freeing memory...\n");
+    halo_free(g_halo);
     single_free(S);
     S.init = 0;
 }

@@ -20,57 +20,9 @@
 
 #include <vector>
 
-#include <rccl/rccl.h>
-
 #include "../../include/mceik.h"
+#include "rccl_rt.h"
 #include "mcmc_common.h"
-
-namespace {
-
-struct Rccl {
-    bool ok = false;
-    const char *(*GetErrorString)(ncclResult_t);
-    ncclResult_t (*GetUniqueId)(ncclUniqueId *);
-    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
-    ncclResult_t (*CommDestroy)(ncclComm_t);
-    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
-    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
-    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
-    ncclResult_t (*GroupStart)();
-    ncclResult_t (*GroupEnd)();
-};
-
-const Rccl &rccl()
-{
-    static Rccl r = [] {
-        Rccl x;
-        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) {
-            fprintf(stderr, "mceik_comm: cannot load RCCL (%s)\n", dlerror());
-            return x;
-        }
-        bool all = true;
-        auto get = [&](auto &fn, const char *name) {
-            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
-            if (!fn) { fprintf(stderr, "mceik_comm: RCCL lacks %s\n", name); all = false; }
-        };
-        get(x.GetErrorString, "ncclGetErrorString");
-        get(x.GetUniqueId, "ncclGetUniqueId");
-        get(x.CommInitRank, "ncclCommInitRank");
-        get(x.CommDestroy, "ncclCommDestroy");
-        get(x.AllGather, "ncclAllGather");
-        get(x.Send, "ncclSend");
-        get(x.Recv, "ncclRecv");
-        get(x.GroupStart, "ncclGroupStart");
-        get(x.GroupEnd, "ncclGroupEnd");
-        x.ok = all;
-        return x;
-    }();
-    return r;
-}
-
-}  // namespace
 
 // Runs the calling scope on `dev` and restores the caller's device.
 struct DevScope {
@@ -109,7 +61,7 @@ struct mceik_comm {
     do {                                                                                   \
         ncclResult_t r_ = (x);                                                             \
         if (r_ != ncclSuccess) {                                                           \
-            fprintf(stderr, "mceik_comm: %s failed: %s\n", #x, rccl().GetErrorString(r_)); \
+            fprintf(stderr, "mceik_comm: %s failed: %s\n", #x, mceik_rccl().GetErrorString(r_)); \
             return -1;                                                                     \
         }                                                                                  \
     } while (0)
@@ -125,9 +77,9 @@ struct mceik_comm {
 extern "C" int mceik_comm_unique_id(unsigned char id[MCEIK_COMM_ID_BYTES])
 {
     static_assert(sizeof(ncclUniqueId) == MCEIK_COMM_ID_BYTES, "RCCL id size");
-    if (!id || !rccl().ok) return 1;
+    if (!id || !mceik_rccl().ok) return 1;
     ncclUniqueId u;
-    RCCLCHK(rccl().GetUniqueId(&u));
+    RCCLCHK(mceik_rccl().GetUniqueId(&u));
     memcpy(id, &u, sizeof(u));
     return 0;
 }
@@ -135,22 +87,22 @@ extern "C" int mceik_comm_unique_id(unsigned char id[MCEIK_COMM_ID_BYTES])
 extern "C" int mceik_comm_init(const unsigned char id[MCEIK_COMM_ID_BYTES], int nranks, int rank, int device,
                                mceik_comm **out)
 {
-    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || !rccl().ok) return 1;
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks || !mceik_rccl().ok) return 1;
     *out = nullptr;
     DevScope dg(device);
     mceik_comm *c = new mceik_comm();
     c->nranks = nranks; c->rank = rank; c->device = device;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
-    ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, u, rank);
+    ncclResult_t r = mceik_rccl().CommInitRank(&c->comm, nranks, u, rank);
     hipError_t e = r == ncclSuccess ? hipMalloc(&c->d_shard, (size_t)nranks * 3 * sizeof(int)) : hipSuccess;
     if (r == ncclSuccess && e == hipSuccess) {
         e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
         if (e != hipSuccess) hipFree(c->d_shard);
     }
     if (r != ncclSuccess || e != hipSuccess) {
-        fprintf(stderr, "mceik_comm_init: %s\n", r != ncclSuccess ? rccl().GetErrorString(r) : hipGetErrorString(e));
-        if (r == ncclSuccess) rccl().CommDestroy(c->comm);
+        fprintf(stderr, "mceik_comm_init: %s\n", r != ncclSuccess ? mceik_rccl().GetErrorString(r) : hipGetErrorString(e));
+        if (r == ncclSuccess) mceik_rccl().CommDestroy(c->comm);
         delete c;
         return -1;
     }
@@ -166,7 +118,7 @@ extern "C" int mceik_comm_finalize(mceik_comm **pc)
     {
         DevScope dg(c->device);
         hipStreamSynchronize(c->stream);
-        r = rccl().CommDestroy(c->comm);
+        r = mceik_rccl().CommDestroy(c->comm);
         hipStreamDestroy(c->stream);
         hipFree(c->d_shard);
     }
@@ -228,7 +180,7 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
     const int mine[3] = {sh.chain_offset, have ? sh.nchains : -1, status};
     std::vector<int> all((size_t)c->nranks * 3);
     if (hipMemcpy(c->d_shard + 3 * c->rank, mine, sizeof(mine), hipMemcpyHostToDevice) != hipSuccess ||
-        rccl().AllGather(c->d_shard + 3 * c->rank, c->d_shard, 3, ncclInt32, c->comm, st) != ncclSuccess ||
+        mceik_rccl().AllGather(c->d_shard + 3 * c->rank, c->d_shard, 3, ncclInt32, c->comm, st) != ncclSuccess ||
         hipStreamSynchronize(st) != hipSuccess ||
         hipMemcpy(all.data(), c->d_shard, all.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
         fprintf(stderr, "mceik_mcmc_gather: the shard-table all-gather failed\n");
@@ -260,19 +212,19 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
         }
     }
     // 2. shards to the root (one RCCL group), the root's own by a device copy
-    bool ok = rccl().GroupStart() == ncclSuccess;
+    bool ok = mceik_rccl().GroupStart() == ncclSuccess;
     if (c->rank == root) {
         for (int r = 0; r < c->nranks && ok; r++) {
             if (r == root) continue;
             const size_t off = (size_t)all[3 * r], n = (size_t)all[3 * r + 1];
-            ok = rccl().Recv(d_v + off * ncell, n * ncell, ncclInt32, r, c->comm, st) == ncclSuccess &&
-                 rccl().Recv(d_l + off, n, ncclFloat64, r, c->comm, st) == ncclSuccess;
+            ok = mceik_rccl().Recv(d_v + off * ncell, n * ncell, ncclInt32, r, c->comm, st) == ncclSuccess &&
+                 mceik_rccl().Recv(d_l + off, n, ncclFloat64, r, c->comm, st) == ncclSuccess;
         }
     } else {
-        ok = rccl().Send(sh.v, (size_t)sh.nchains * ncell, ncclInt32, root, c->comm, st) == ncclSuccess &&
-             rccl().Send(sh.logl, (size_t)sh.nchains, ncclFloat64, root, c->comm, st) == ncclSuccess;
+        ok = mceik_rccl().Send(sh.v, (size_t)sh.nchains * ncell, ncclInt32, root, c->comm, st) == ncclSuccess &&
+             mceik_rccl().Send(sh.logl, (size_t)sh.nchains, ncclFloat64, root, c->comm, st) == ncclSuccess;
     }
-    ok = (rccl().GroupEnd() == ncclSuccess) && ok;
+    ok = (mceik_rccl().GroupEnd() == ncclSuccess) && ok;
     if (ok && c->rank == root) {
         const size_t off = (size_t)sh.chain_offset;
         ok = hipMemcpyAsync(d_v + off * ncell, sh.v, (size_t)sh.nchains * ncell * sizeof(int),

@@ -29,11 +29,26 @@ struct BlockDecomp {
     int nd[3], step[3], nov;
 };
 
+// A box of grid nodes [lo, lo + ext) and a list of them packed back to back
+// (box k at off[k] doubles; off[n] = total).
+struct BlockBox {
+    int lo[3], ext[3];
+};
+struct BoxList {
+    int n;
+    BlockBox box[6];
+    size_t off[7];
+};
+
 int fsm_single_occupancy(int is_double);
 hipError_t fsm_single_setbcs(const SingleLaunch &L, const double *d_src, int nsrc, int *d_ierr_bc, hipStream_t st);
+// nblk blocks from b0 (nblk < 0: every block); ierr_b: the block whose
+// last-level ierr is reported
 hipError_t fsm_block_sweep(const SingleLaunch &L, const BlockDecomp &D, const double *snap, int g, int *ierr,
-                           hipStream_t st);
-hipError_t fsm_block_unconverged(const SingleLaunch &L, double tol, unsigned *count, hipStream_t st);
+                           hipStream_t st, int b0 = 0, int nblk = -1, int ierr_b = 0);
+hipError_t fsm_block_unconverged(const SingleLaunch &L, const BlockBox &B, double tol, unsigned *count,
+                                 hipStream_t st);
+hipError_t fsm_box_copy(const SingleLaunch &L, const BoxList &bl, double *buf, int to_buf, hipStream_t st);
 hipError_t fsm_single_solve(const SingleLaunch &L, int is_double, const double *d_src, int nsrc, int *d_ierr_bc,
                             int nwaves, hipStream_t st);
 hipError_t fsm_single_pad(const double *src, void *dst, int is_double, int nx, int ny, int nz, int nxp, int nyp,

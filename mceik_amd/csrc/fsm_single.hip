@@ -25,6 +25,8 @@
 #include <float.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "fsm_common.h"
 #include "fsm_update.h"
 #include "fsm_single.h"
@@ -356,10 +358,17 @@ __global__ void single_pad_kernel(const RS *src, RD *dst, int nx, int ny, int nz
 // workgroup per block walks the block's node hyperplanes in sweep order (the
 // nodes of a level are independent), so the result is bitwise the reference's
 // run with one MPI rank per block.  fp64, the padded layout of SingleLaunch.
+//
+// Across ranks (one block per rank, blocks_solve_ranks in capi.hip) a rank
+// sweeps block b0 alone on a grid whose other nodes change only in the halo
+// swap between sweeps, so snap is u itself.  ierr: the reference's EVAL_UPDATE3D
+// ierr of the last level, the corner node of the rank's local grid (its block
+// extended by the ghost layer, fsm3d.f90:1099-1104), which is an updated node
+// only when the ghost layer does not extend it there (block 0 always).
 __global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockDecomp D, const double *snap, int g,
-                                                          int *ierr)
+                                                          int *ierr, int b0, int ierr_b)
 {
-    const int b = blockIdx.x;
+    const int b = blockIdx.x + b0;
     const int bi[3] = {b % D.nd[0], (b / D.nd[0]) % D.nd[1], b / (D.nd[0] * D.nd[1])};
     const int nn[3] = {L.nx, L.ny, L.nz};
     int lo[3], ext[3];
@@ -373,6 +382,7 @@ __global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockD
     double *u = (double *)L.u;
     const double *slow = (const double *)L.slow;
     const size_t sy = (size_t)L.nxp, sz = (size_t)L.nxp * L.nyp;
+    const bool ierr_here = b == ierr_b && (D.nov == 0 || (lo[0] == 0 && lo[1] == 0 && lo[2] == 0));
     const int nlev = ext[0] + ext[1] + ext[2] - 2;
     for (int lev = 0; lev < nlev; lev++) {
         const int zlo = max(0, lev - (ext[0] - 1) - (ext[1] - 1)), zhi = min(ext[2] - 1, lev);
@@ -402,26 +412,49 @@ __global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockD
             int e;
             const double ub = godunov(ux, uy, uz, slow[idx] * L.h, e);
             u[idx] = self < ub ? self : ub;
-            if (b == 0 && c[0] == 0 && c[1] == 0 && c[2] == 0) *ierr = e;   // rank 0's last EVAL_UPDATE3D
+            if (ierr_here && c[0] == lo[0] && c[1] == lo[1] && c[2] == lo[2]) *ierr = e;   // last level
         }
         __syncthreads();
     }
 }
 
-// nodes with !(|u0 - u| < tol) (the FSM_MPI convergence count, fsm3d.f90:195-205)
-__global__ void block_unconverged_kernel(SingleLaunch L, double tol, unsigned *count)
+// nodes of the box with !(|u0 - u| < tol) (the FSM_MPI convergence count,
+// fsm3d.f90:195-205; the whole grid, or the nodes a rank owns)
+__global__ void block_unconverged_kernel(SingleLaunch L, BlockBox B, double tol, unsigned *count)
 {
-    const size_t n = (size_t)L.nx * L.ny * L.nz;
+    const size_t n = (size_t)B.ext[0] * B.ext[1] * B.ext[2];
     unsigned c = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const int x = (int)(i % L.nx);
-        const size_t t = i / L.nx;
-        const int y = (int)(t % L.ny), z = (int)(t / L.ny);
+        const int x = B.lo[0] + (int)(i % B.ext[0]);
+        const size_t t = i / B.ext[0];
+        const int y = B.lo[1] + (int)(t % B.ext[1]), z = B.lo[2] + (int)(t / B.ext[1]);
         const size_t p = ((size_t)z * L.nyp + y) * L.nxp + x;
         const double d = ((const double *)L.u0)[p] - ((const double *)L.u)[p];
         c += !(__builtin_fabs(d) < tol);
     }
     if (c) atomicAdd(count, c);
+}
+
+// Boxes of the padded fp64 grid <-> one contiguous buffer, box k at off[k],
+// x fastest inside a box: the halo faces a rank swaps after every sweep
+// (EIKONAL_EXCHANGE, fsm3d.f90:971-1046) and the owned block it sends to the
+// master at the end (EIKONAL_GATHER_TRAVELTIMES).
+__global__ void box_copy_kernel(SingleLaunch L, BoxList bl, double *buf, int to_buf)
+{
+    const size_t total = bl.off[bl.n];
+    double *u = (double *)L.u;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        int k = 0;
+        while (i >= bl.off[k + 1]) k++;
+        const BlockBox &B = bl.box[k];
+        const size_t j = i - bl.off[k];
+        const int x = B.lo[0] + (int)(j % B.ext[0]);
+        const size_t t = j / B.ext[0];
+        const int y = B.lo[1] + (int)(t % B.ext[1]), z = B.lo[2] + (int)(t / B.ext[1]);
+        const size_t p = ((size_t)z * L.nyp + y) * L.nxp + x;
+        if (to_buf) buf[i] = u[p];
+        else u[p] = buf[i];
+    }
 }
 
 }  // namespace
@@ -435,15 +468,28 @@ hipError_t fsm_single_setbcs(const SingleLaunch &L, const double *d_src, int nsr
 }
 
 hipError_t fsm_block_sweep(const SingleLaunch &L, const BlockDecomp &D, const double *snap, int g, int *ierr,
-                           hipStream_t st)
+                           hipStream_t st, int b0, int nblk, int ierr_b)
 {
-    hipLaunchKernelGGL(block_sweep_kernel, dim3(D.nd[0] * D.nd[1] * D.nd[2]), dim3(256), 0, st, L, D, snap, g, ierr);
+    if (nblk < 0) nblk = D.nd[0] * D.nd[1] * D.nd[2];
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(block_sweep_kernel, dim3(nblk), dim3(256), 0, st, L, D, snap, g, ierr, b0, ierr_b);
     return hipGetLastError();
 }
 
-hipError_t fsm_block_unconverged(const SingleLaunch &L, double tol, unsigned *count, hipStream_t st)
+hipError_t fsm_block_unconverged(const SingleLaunch &L, const BlockBox &B, double tol, unsigned *count,
+                                 hipStream_t st)
 {
-    hipLaunchKernelGGL(block_unconverged_kernel, dim3(512), dim3(256), 0, st, L, tol, count);
+    if ((size_t)B.ext[0] * B.ext[1] * B.ext[2] == 0) return hipSuccess;
+    hipLaunchKernelGGL(block_unconverged_kernel, dim3(512), dim3(256), 0, st, L, B, tol, count);
+    return hipGetLastError();
+}
+
+hipError_t fsm_box_copy(const SingleLaunch &L, const BoxList &bl, double *buf, int to_buf, hipStream_t st)
+{
+    if (bl.n < 1 || bl.off[bl.n] == 0) return hipSuccess;
+    const size_t total = bl.off[bl.n];
+    const unsigned nblk = (unsigned)std::min<size_t>(1024, (total + 255) / 256);
+    hipLaunchKernelGGL(box_copy_kernel, dim3(nblk), dim3(256), 0, st, L, bl, buf, to_buf);
     return hipGetLastError();
 }
 

@@ -29,12 +29,22 @@
 typedef int (*flag_fn)(int *);
 typedef int (*rank_fn)(MPI_Comm, int *);
 typedef int (*bcast_fn)(void *, int, MPI_Datatype, int, MPI_Comm);
+typedef int (*allreduce_fn)(const void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
+typedef int (*allgather_fn)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, MPI_Comm);
+typedef int (*isend_fn)(const void *, int, MPI_Datatype, int, int, MPI_Comm, MPI_Request *);
+typedef int (*irecv_fn)(void *, int, MPI_Datatype, int, int, MPI_Comm, MPI_Request *);
+typedef int (*waitall_fn)(int, MPI_Request *, MPI_Status *);
 
 static struct {
     int tried, ok;
     flag_fn initialized, finalized;
-    rank_fn rank;
+    rank_fn rank, size;
     bcast_fn bcast;
+    allreduce_fn allreduce;
+    allgather_fn allgather;
+    isend_fn isend;
+    irecv_fn irecv;
+    waitall_fn waitall;
 } rt;
 
 static void *sym(void *h, const char *name)
@@ -52,8 +62,15 @@ static int load(void)
         rt.initialized = (flag_fn)sym(h, "MPI_Initialized");
         rt.finalized = (flag_fn)sym(h, "MPI_Finalized");
         rt.rank = (rank_fn)sym(h, "MPI_Comm_rank");
+        rt.size = (rank_fn)sym(h, "MPI_Comm_size");
         rt.bcast = (bcast_fn)sym(h, "MPI_Bcast");
-        rt.ok = rt.initialized && rt.finalized && rt.rank && rt.bcast;
+        rt.allreduce = (allreduce_fn)sym(h, "MPI_Allreduce");
+        rt.allgather = (allgather_fn)sym(h, "MPI_Allgather");
+        rt.isend = (isend_fn)sym(h, "MPI_Isend");
+        rt.irecv = (irecv_fn)sym(h, "MPI_Irecv");
+        rt.waitall = (waitall_fn)sym(h, "MPI_Waitall");
+        rt.ok = rt.initialized && rt.finalized && rt.rank && rt.size && rt.bcast && rt.allreduce && rt.allgather &&
+                rt.isend && rt.irecv && rt.waitall;
     }
     if (!rt.ok) return 0;
     int a = 0, b = 0;
@@ -80,6 +97,53 @@ MCEIK_HIDDEN int mceik_mpi_bcast_double(int fcomm, double *v, int n, int root)
     if (!load()) return -1;
     return rt.bcast(v, n, MPI_DOUBLE, root, MPI_Comm_f2c((MPI_Fint)fcomm)) == MPI_SUCCESS ? 0 : -1;
 }
+
+/* The block-decomposed solve across ranks (fsm3d.f90:103-222 with
+ * EIKONAL_EXCHANGE :971-1046 and the gather of EIKONAL_GATHER_TRAVELTIMES):
+ * communicator size, an integer all-reduce (op 0 sum, 1 max), an all-gather of
+ * fixed-size byte records, and a batch of non-blocking double sends/receives
+ * completed together (the halo swap: every rank posts all of its faces, so no
+ * ordering can deadlock). */
+MCEIK_HIDDEN int mceik_mpi_size(int fcomm)
+{
+    if (!load()) return -1;
+    int n = -1;
+    return rt.size(MPI_Comm_f2c((MPI_Fint)fcomm), &n) == MPI_SUCCESS ? n : -1;
+}
+
+MCEIK_HIDDEN int mceik_mpi_allreduce_int(int fcomm, int *v, int n, int op)
+{
+    if (!load()) return -1;
+    return rt.allreduce(MPI_IN_PLACE, v, n, MPI_INT, op ? MPI_MAX : MPI_SUM, MPI_Comm_f2c((MPI_Fint)fcomm)) ==
+                   MPI_SUCCESS ? 0 : -1;
+}
+
+MCEIK_HIDDEN int mceik_mpi_allgather_bytes(int fcomm, const void *mine, void *all, int nbytes)
+{
+    if (!load()) return -1;
+    return rt.allgather(mine, nbytes, MPI_BYTE, all, nbytes, MPI_BYTE, MPI_Comm_f2c((MPI_Fint)fcomm)) ==
+                   MPI_SUCCESS ? 0 : -1;
+}
+
+/* nmsg messages: send[k] (count[k] doubles to peer[k], tag tag[k]) when
+ * dir[k] = 0, receive (from peer[k]) when dir[k] = 1; all complete on return. */
+MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, const int *peer, const int *tag,
+                                           double *const *buf, const int *count)
+{
+    if (!load()) return -1;
+    if (nmsg <= 0) return 0;
+    if (nmsg > 64) return -1;
+    MPI_Comm c = MPI_Comm_f2c((MPI_Fint)fcomm);
+    MPI_Request req[64];
+    int bad = 0;
+    for (int k = 0; k < nmsg; k++) {
+        const int r = dir[k] ? rt.irecv(buf[k], count[k], MPI_DOUBLE, peer[k], tag[k], c, &req[k])
+                             : rt.isend(buf[k], count[k], MPI_DOUBLE, peer[k], tag[k], c, &req[k]);
+        if (r != MPI_SUCCESS) { req[k] = MPI_REQUEST_NULL; bad = 1; }
+    }
+    if (rt.waitall(nmsg, req, MPI_STATUSES_IGNORE) != MPI_SUCCESS) bad = 1;
+    return bad ? -1 : 0;
+}
 #else
 MCEIK_HIDDEN int mceik_mpi_rank(int fcomm) { (void)fcomm; return -1; }
 MCEIK_HIDDEN int mceik_mpi_bcast_int(int fcomm, int *v, int n, int root)
@@ -90,6 +154,23 @@ MCEIK_HIDDEN int mceik_mpi_bcast_int(int fcomm, int *v, int n, int root)
 MCEIK_HIDDEN int mceik_mpi_bcast_double(int fcomm, double *v, int n, int root)
 {
     (void)fcomm; (void)v; (void)n; (void)root;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_size(int fcomm) { (void)fcomm; return -1; }
+MCEIK_HIDDEN int mceik_mpi_allreduce_int(int fcomm, int *v, int n, int op)
+{
+    (void)fcomm; (void)v; (void)n; (void)op;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_allgather_bytes(int fcomm, const void *mine, void *all, int nbytes)
+{
+    (void)fcomm; (void)mine; (void)all; (void)nbytes;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, const int *peer, const int *tag,
+                                           double *const *buf, const int *count)
+{
+    (void)fcomm; (void)nmsg; (void)dir; (void)peer; (void)tag; (void)buf; (void)count;
     return -1;
 }
 #endif

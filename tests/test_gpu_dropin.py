@@ -300,3 +300,99 @@ def test_mpi_variant_blocks_xfsm3d_digest():
                            [0.0] + [100.0 * v / 2.0 for v in n])
     assert ierr == 0 and u.max() == 1.4308203212738235
     assert hashlib.sha256(u.tobytes()).hexdigest() == str(d["xfsm3d_sha256"])
+
+
+@pytest.fixture(scope="module")
+def blocks_mpi_exe(tmp_path_factory):
+    _dev()
+    mpi = "/opt/conda"
+    if not (os.path.exists(f"{mpi}/bin/mpiexec") and os.path.exists(f"{mpi}/lib/libmpi.so")):
+        pytest.skip("no MPI toolchain in this image")
+    exe = str(tmp_path_factory.mktemp("bmpi") / "blocks_mpi_gpu")
+    lib = os.path.join(ROOT, "mceik_amd")
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), "-I", f"{mpi}/include",
+                    os.path.join(ROOT, "tests", "c", "blocks_mpi_gpu.c"), "-L", lib, "-lmceik_hip",
+                    f"{mpi}/lib/libmpi.so", f"-Wl,-rpath,/usr/lib/x86_64-linux-gnu:{lib}:{mpi}/lib", "-lm",
+                    "-o", exe], check=True)
+    return f"{mpi}/bin/mpiexec", exe
+
+
+def _run_blocks_ranks(blocks_mpi_exe, tmp_path, n3, nd, nov, maxit, tol, h, slow, src):
+    mpiexec, exe = blocks_mpi_exe
+    sp, op = str(tmp_path / "slow.f64"), str(tmp_path / "u.f64")
+    np.ascontiguousarray(slow, dtype=np.float64).tofile(sp)
+    cmd = [mpiexec, "-n", str(nd[0] * nd[1] * nd[2]), exe, *map(str, n3), *map(str, nd), str(nov), str(maxit),
+           repr(tol), repr(h), "0", "0", "0", *map(repr, (float(v) for v in src)), sp, op]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    print(out.stdout[-3000:], out.stderr[-2000:])
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    ranks = {int(ln.split()[1]): int(ln.split()[3]) for ln in out.stdout.splitlines() if ln.startswith("rank ")}
+    assert sorted(ranks) == list(range(nd[0] * nd[1] * nd[2]))
+    res = np.fromfile(op)
+    return res[:-1], int(res[-1]), ranks
+
+
+@pytest.mark.parametrize("case", _blocks_golden()[1])
+def test_mpi_variant_blocks_across_ranks_bitwise_vs_reference(blocks_mpi_exe, tmp_path, case):
+    """The distributed MPI variant (one rank per block, each sweeping its block
+    on the GPU and swapping face layers with its neighbours after every sweep
+    -- host-staged MPI here, the ranks sharing one GPU -- the master gathering
+    u) under mpiexec with ndivx*ndivy*ndivz ranks: u and the master's ierr
+    bitwise = the reference's own run with the same ranks and arguments
+    (tests/golden/blocks_mpi.npz); SETBCS's error reaches every rank."""
+    d, _ = _blocks_golden()
+    cfg = d[f"{case}_cfg"]
+    nd = tuple(int(v) for v in cfg[:3])
+    u, ierr, ranks = _run_blocks_ranks(blocks_mpi_exe, tmp_path, tuple(int(v) for v in d["grid"]), nd, int(cfg[3]),
+                                       int(cfg[4]), 1e-8, float(d["h"]), d["slow"], d[f"{case}_src"])
+    assert ierr == ranks[0] == int(d[f"{case}_ierr"])
+    if case.endswith("_err"):
+        assert all(e == 1 for e in ranks.values()), ranks
+    if f"{case}_u" in d.files:
+        assert np.array_equal(u.view(np.uint64), d[f"{case}_u"].view(np.uint64))
+
+
+def test_mpi_variant_xfsm3d_eight_ranks_digest(blocks_mpi_exe, tmp_path):
+    """The reference's xfsm3d case (70x80x90, 2x2x2 blocks, maxit 5, tol 1e-7)
+    on 8 ranks, one block each: the gathered field's sha256 equals the
+    reference's 8-rank MPI run."""
+    import hashlib
+    d, _ = _blocks_golden()
+    n3 = (70, 80, 90)
+    u, ierr, ranks = _run_blocks_ranks(blocks_mpi_exe, tmp_path, n3, (2, 2, 2), 1, 5, 1e-7, 100.0,
+                                       np.full(n3[0] * n3[1] * n3[2], 1.0 / 5.0e3),
+                                       [0.0] + [100.0 * v / 2.0 for v in n3])
+    assert ierr == 0 and u.max() == float(d["xfsm3d_max"]) == 1.4308203212738235
+    assert hashlib.sha256(u.tobytes()).hexdigest() == str(d["xfsm3d_sha256"])
+
+
+def test_mpi_variant_uneven_blocks_across_ranks_vs_one_gpu(blocks_mpi_exe, tmp_path):
+    """A 3 x 2 x 1 decomposition with uneven blocks (the last block takes the
+    remainder, fsm3d.f90:1096-1098) and a two-node ghost layer on 6 ranks:
+    bitwise = the same decomposition run on one GPU (the single-process block
+    iteration pinned by the reference goldens above)."""
+    d, _ = _blocks_golden()
+    n3 = tuple(int(v) for v in d["grid"])
+    src = d["b222_src"]
+    u, ierr, ranks = _run_blocks_ranks(blocks_mpi_exe, tmp_path, n3, (3, 2, 1), 2, 50, 1e-8, float(d["h"]),
+                                       d["slow"], src)
+    u1, e1 = _mpi_variant(*n3, (3, 2, 1), 2, 50, 1e-8, float(d["h"]), d["slow"], src)
+    assert ierr == e1 == 0
+    assert np.array_equal(u.view(np.uint64), u1.view(np.uint64))
+
+
+def test_mpi_variant_rccl_halo_refused_on_shared_gpu(blocks_mpi_exe, tmp_path):
+    """MCEIK_HALO=rccl with two ranks on one GPU: RCCL refuses the
+    communicator (one rank per GPU), and initialize returns ierr = 1 on both
+    ranks together instead of leaving one waiting in a collective."""
+    mpiexec, exe = blocks_mpi_exe
+    d, _ = _blocks_golden()
+    sp = str(tmp_path / "slow.f64")
+    d["slow"].tofile(sp)
+    env = dict(os.environ, MCEIK_HALO="rccl")
+    out = subprocess.run([mpiexec, "-n", "2", exe, *map(str, d["grid"]), "2", "1", "1", "1", "50", "1e-8", "100",
+                          "0", "0", "0", "0", "834.5", "987.6", "1100", sp, str(tmp_path / "u.f64")],
+                         capture_output=True, text=True, timeout=120, env=env)
+    print(out.stdout[-2000:], out.stderr[-2000:])
+    assert out.returncode == 0
+    assert "rank 0 init_ierr 1" in out.stdout and "rank 1 init_ierr 1" in out.stdout
