@@ -45,7 +45,7 @@ struct FsmLaunch {
     int *niter;                  // [nsolve] iterations executed, may be null
     int *ierr;                   // [nsolve] reference ierr semantics, may be null
     int cell_cache;              // slow_mode 1: every tile's cells fit the LDS cell cache
-    int fast_sqrt;               // host-validated: f = s*h is a normal float >= 1e-18
+    int fast_sqrt;               // host-validated: f = s*h >= 1e-12 (sqrt_normal is exact for x >= 2^-104, profiles/r03_sqrt)
     unsigned *counter;           // 8 work-queue heads, 128 B apart (zeroed before the launch)
     unsigned long long *iter_total;   // += iterations of every solve (roofline accounting), may be null
     unsigned long long *visit_stats;  // [4] += brick visits, column-segment updates, changed segments, macro steps; may be null

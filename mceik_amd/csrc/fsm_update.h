@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
+#ifndef MCEIK_SQRT_ADD3_ASM
+#define MCEIK_SQRT_ADD3_ASM 0     // 1: the add as an asm statement too (the compiler pads its use: +0.2% slower, tools A/B)
+#endif
 #ifndef MCEIK_SQRT_INT
 #define MCEIK_SQRT_INT 1     // sqrt_normal's rounding choice in integer arithmetic (0: compares + selects)
 #endif
@@ -113,9 +116,21 @@ __device__ __forceinline__ float sqrt_normal(float x)
 #if MCEIK_SQRT_INT
     // (asm: the instruction selector turns the clamp back into compares + carry adds)
     int pdn, pup, r;
+#if MCEIK_SQRT_ADD3_ASM == 2
+    // one asm statement: the compiler pads a use of an asm result by a wait
+    // state (it cannot see whether the asm wrote a transcendental result), so
+    // the three instructions are one block and only r's use can be padded
+    asm("v_med3_i32 %1, %3, 0, 1\n\tv_med3_i32 %2, %4, 0, 1\n\tv_add3_u32 %0, %5, %1, %2"
+        : "=v"(r), "=&v"(pdn), "=&v"(pup) : "v"(edn), "v"(eup), "v"(sb - 1));
+#else
     asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pdn) : "v"(edn));
     asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pup) : "v"(eup));
+#if MCEIK_SQRT_ADD3_ASM
     asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(sb - 1), "v"(pdn), "v"(pup));
+#else
+    r = (sb - 1) + pdn + pup;           // v_add3_u32 from the selector
+#endif
+#endif
     return __builtin_bit_cast(float, r);
 #else
     const float t = __builtin_bit_cast(float, edn) <= 0.0f ? dn : s;
