@@ -45,9 +45,9 @@ void eikonal3d_serial_driver_sp(const int *job, const int *iverb, const int *max
  * (EIKONAL3D_FSM_MPI: each block sweeps its nodes against ghost copies
  * refreshed after every sweep), so u and ierr are bitwise the reference's run
  * with one MPI rank per block; one block = the serial driver's solve.  With
- * as many ranks in comm as blocks (the reference's layout) every rank sweeps
- * its own block on its GPU and swaps face layers with its neighbours after
- * every sweep (RCCL when each rank has a GPU of its own, host-staged MPI when
+ * as many ranks in comm as blocks (the reference's layout) every rank holds
+ * only its block and the ghost layer on its GPU, sweeps the block and swaps
+ * face layers with its neighbours after every sweep (RCCL when each rank has a GPU of its own, host-staged MPI when
  * ranks share one; MCEIK_HALO=mpi|rccl), and the master gathers u; otherwise
  * the master's GPU runs every block.  The master passes the full arrays
  * (n = nx*ny*nz) and receives u; the other ranks pass n = 1 as the

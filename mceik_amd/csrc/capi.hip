@@ -466,6 +466,7 @@ static int single_alloc(SingleState &S, int is_double, int nx, int ny, int nz, i
     if (nx < 1 || ny < 1 || nz < 1 || (long)nx * ny * nz >= (1L << 31)) return 1;
     SingleLaunch &L = S.L;
     L.nx = nx; L.ny = ny; L.nz = nz;
+    L.gx = nx; L.gy = ny; L.gz = nz;             // the whole grid (rank_alloc: a box of it)
     L.nbx = mceik_div_up(nx, 8); L.nby = mceik_div_up(ny, 8); L.nbz = mceik_div_up(nz, 8);
     if (L.nbx > 1024 || L.nby > 1024 || L.nbz > 1024) return 1;
     L.nxp = 8 * L.nbx; L.nyp = 8 * L.nby; L.nzp = 8 * L.nbz;
@@ -738,7 +739,9 @@ extern "C" int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, co
 struct RankHalo {
     int on;                      // the solve runs one block per rank
     int fcomm, rank, nranks;
+    int gn[3];                   // the global grid
     BlockBox own;                // the block this rank owns (= its rank)
+    BlockBox hbox;               // the nodes this rank holds: its block and the ghost layer
     int kind;                    // 1: host-staged MPI, 2: RCCL
     int peer[6], tag_send[6], tag_recv[6];
     BoxList send, recv;          // faces sent / received, in the same face order
@@ -772,6 +775,33 @@ static bool decomp_tiles(const BlockDecomp &D, const int nn[3])
     return tot == (long long)nn[0] * nn[1] * nn[2];
 }
 
+// The nodes rank r holds: its block extended by the one-node ghost layer the
+// sweep reads (clamped to the grid); a 1-node dummy for an empty block.
+static BlockBox halo_box(const BlockDecomp &D, const int nn[3], int r)
+{
+    int lo[3], ext[3];
+    decomp_block(D, nn, r, lo, ext);
+    BlockBox b{{0, 0, 0}, {1, 1, 1}};
+    if (ext[0] <= 0 || ext[1] <= 0 || ext[2] <= 0) return b;
+    for (int a = 0; a < 3; a++) {
+        const int l = std::max(0, lo[a] - 1), h = std::min(nn[a] - 1, lo[a] + ext[a]);
+        b.lo[a] = l;
+        b.ext[a] = h - l + 1;
+    }
+    return b;
+}
+
+// Device state of a rank's box (reallocated when nsrc outgrows it): the
+// fields hold hbox of the global grid.
+static int rank_alloc(SingleState &S, const RankHalo &H, int maxit, int nsrc)
+{
+    if (single_alloc(S, 1, H.hbox.ext[0], H.hbox.ext[1], H.hbox.ext[2], maxit, nsrc)) return 1;
+    SingleLaunch &L = S.L;
+    L.gx = H.gn[0]; L.gy = H.gn[1]; L.gz = H.gn[2];
+    L.ox = H.hbox.lo[0]; L.oy = H.hbox.lo[1]; L.oz = H.hbox.lo[2];
+    return 0;
+}
+
 static void halo_free(RankHalo &H)
 {
     if (H.nc) mceik_rccl().CommDestroy(H.nc);
@@ -786,6 +816,8 @@ static int halo_setup(RankHalo &H, const BlockDecomp &D, const int nn[3], int fc
 {
     halo_free(H);
     H.fcomm = fcomm; H.rank = rank; H.nranks = nranks;
+    for (int a = 0; a < 3; a++) H.gn[a] = nn[a];
+    H.hbox = halo_box(D, nn, rank);
     int lo[3], ext[3];
     decomp_block(D, nn, rank, lo, ext);
     for (int a = 0; a < 3; a++) { H.own.lo[a] = lo[a]; H.own.ext[a] = ext[a]; }
@@ -908,39 +940,79 @@ static int halo_swap(RankHalo &H, const SingleLaunch &L, hipStream_t st, int fai
     return fail;
 }
 
+// Node box B (global coordinates) of the dense x-fastest grid g <-> a packed
+// x-fastest buffer (host side of the model scatter and the field gather).
+static void host_box(double *grid, const int g[3], const BlockBox &B, double *buf, bool to_buf)
+{
+    size_t i = 0;
+    for (int z = 0; z < B.ext[2]; z++)
+        for (int y = 0; y < B.ext[1]; y++) {
+            double *row = grid + ((size_t)(B.lo[2] + z) * g[1] + B.lo[1] + y) * g[0] + B.lo[0];
+            if (to_buf) memcpy(buf + i, row, (size_t)B.ext[0] * 8);
+            else memcpy(row, buf + i, (size_t)B.ext[0] * 8);
+            i += B.ext[0];
+        }
+}
+static size_t box_count(const BlockBox &B)
+{
+    return B.ext[0] > 0 && B.ext[1] > 0 && B.ext[2] > 0 ? (size_t)B.ext[0] * B.ext[1] * B.ext[2] : 0;
+}
+
 // The distributed solve (collective over comm; the master's slow/u are the
-// whole grid, the others' are not read or written).  Every rank returns its own
-// ierr as the reference's (SETBCS: the same on every rank; the solver: the
+// whole grid, the others' are not read or written).  The master sends every
+// rank the slowness of the nodes it holds (EIKONAL_SCATTER_MODEL) and the
+// sources; every rank runs SETBCS on its box (the same nodes and values as on
+// the whole grid), sweeps its block with a face swap after every sweep, and
+// sends its block back (EIKONAL_GATHER_TRAVELTIMES).  Every rank returns its
+// own ierr as the reference's (SETBCS: the same on every rank; the solver: the
 // ierr of its local grid's last level), -1 on a failure on any rank.
 static int blocks_solve_ranks(SingleState &S, RankHalo &H, int nsrc, const double *ts, const double *xs,
                               const double *ys, const double *zs, const double *slow, double *u)
 {
     SingleLaunch &L = S.L;
-    const size_t n = (size_t)L.nx * L.ny * L.nz, np = (size_t)L.nxp * L.nyp * L.nzp;
+    const size_t nloc = (size_t)L.nx * L.ny * L.nz, np = (size_t)L.nxp * L.nyp * L.nzp;
     L.maxit = S.maxit; L.tol = S.tol; L.h = S.h; L.x0 = S.x0; L.y0 = S.y0; L.z0 = S.z0;
     const bool master = H.rank == 0;
-    // the master's model and sources on every rank (EIKONAL_SCATTER_MODEL's role)
-    std::vector<double> src((size_t)nsrc * 4), mslow(master ? 0 : n);
+    std::vector<double> src((size_t)nsrc * 4), mine(nloc);
     if (master)
         for (int k = 0; k < nsrc; k++) {
             src[k * 4 + 0] = ts[k]; src[k * 4 + 1] = xs[k]; src[k * 4 + 2] = ys[k]; src[k * 4 + 3] = zs[k];
         }
-    const double *sl = master ? slow : mslow.data();
-    if (mceik_mpi_bcast_double(H.fcomm, src.data(), nsrc * 4, 0) ||
-        mceik_mpi_bcast_double(H.fcomm, (double *)sl, (int)n, 0))
-        return -1;
+    if (mceik_mpi_bcast_double(H.fcomm, src.data(), nsrc * 4, 0)) return -1;
+    int fail = 0;
+    {   // the slowness of every rank's box from the master
+        std::vector<std::vector<double>> out;
+        std::vector<int> dir, peer, tag, cnt;
+        std::vector<double *> buf;
+        if (master) {
+            host_box((double *)slow, H.gn, H.hbox, mine.data(), true);
+            out.resize(H.nranks);
+            for (int r = 1; r < H.nranks; r++) {
+                const BlockBox b = halo_box(S.D, H.gn, r);
+                out[r].resize(box_count(b));
+                host_box((double *)slow, H.gn, b, out[r].data(), true);
+                dir.push_back(0); peer.push_back(r); tag.push_back(98); cnt.push_back((int)out[r].size());
+                buf.push_back(out[r].data());
+            }
+        } else {
+            dir.push_back(1); peer.push_back(0); tag.push_back(98); cnt.push_back((int)nloc); buf.push_back(mine.data());
+        }
+        if (mceik_mpi_exchange_double(H.fcomm, (int)dir.size(), dir.data(), peer.data(), tag.data(), buf.data(),
+                                      cnt.data()))
+            return -1;
+    }
     hipStream_t st = S.st;
     const BlockBox own = H.own;
     const bool empty = own.ext[0] <= 0 || own.ext[1] <= 0 || own.ext[2] <= 0;
-    int fail = 0, ierr_bc = 0, ierr = 0;
-    if (hipMemcpyAsync(S.dense, sl, n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+    int ierr_bc = 0, ierr = 0;
+    if (hipMemcpyAsync(S.dense, mine.data(), nloc * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(S.src, src.data(), src.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
         fsm_single_pad(S.dense, (void *)L.slow, 1, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
         fsm_single_setbcs(L, S.src, nsrc, S.ierr_bc, st) != hipSuccess ||
         hipMemcpyAsync(&ierr_bc, S.ierr_bc, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         fail = 1;
-    int agree[2] = {fail, ierr_bc};                  // SETBCS runs alike everywhere; the master's error counts
+    int agree[2] = {fail, ierr_bc};                  // SETBCS's checks run alike everywhere
     if (mceik_mpi_allreduce_int(H.fcomm, agree, 2, 1)) return -1;
     if (agree[0]) return -1;
     S.bcfail = agree[1] != 0;
@@ -968,50 +1040,40 @@ static int blocks_solve_ranks(SingleState &S, RankHalo &H, int nsrc, const doubl
         if (tot[0] == 0) break;
     }
     // every block to the master
-    BoxList mine;
-    mine.n = 1; mine.box[0] = own; mine.off[0] = 0;
-    mine.off[1] = empty ? 0 : (size_t)own.ext[0] * own.ext[1] * own.ext[2];
-    if (master) {
+    BoxList bl;
+    bl.n = 1; bl.box[0] = own; bl.off[0] = 0; bl.off[1] = empty ? 0 : box_count(own);
+    std::vector<double> blk(bl.off[1]);
+    if (!fail && bl.off[1] &&
+        (fsm_box_copy(L, bl, S.dense, 1, st) != hipSuccess ||
+         hipMemcpyAsync(blk.data(), S.dense, blk.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+         hipStreamSynchronize(st) != hipSuccess))
+        fail = 1;
+    {
         std::vector<std::vector<double>> got(H.nranks);
+        std::vector<BlockBox> box(H.nranks);
         std::vector<int> dir, peer, tag, cnt;
         std::vector<double *> buf;
-        std::vector<BlockBox> box(H.nranks);
-        const int nn[3] = {L.nx, L.ny, L.nz};
-        for (int r = 1; r < H.nranks; r++) {
-            int lo[3], ext[3];
-            decomp_block(S.D, nn, r, lo, ext);
-            for (int a = 0; a < 3; a++) { box[r].lo[a] = lo[a]; box[r].ext[a] = ext[a] > 0 ? ext[a] : 0; }
-            const size_t c = (size_t)box[r].ext[0] * box[r].ext[1] * box[r].ext[2];
-            if (!c) continue;
-            got[r].resize(c);
-            dir.push_back(1); peer.push_back(r); tag.push_back(99); cnt.push_back((int)c); buf.push_back(got[r].data());
+        if (master) {
+            for (int r = 1; r < H.nranks; r++) {
+                int lo[3], ext[3];
+                decomp_block(S.D, H.gn, r, lo, ext);
+                for (int a = 0; a < 3; a++) { box[r].lo[a] = lo[a]; box[r].ext[a] = ext[a]; }
+                got[r].resize(box_count(box[r]));
+                if (got[r].empty()) continue;
+                dir.push_back(1); peer.push_back(r); tag.push_back(99); cnt.push_back((int)got[r].size());
+                buf.push_back(got[r].data());
+            }
+        } else if (!blk.empty()) {
+            dir.push_back(0); peer.push_back(0); tag.push_back(99); cnt.push_back((int)blk.size()); buf.push_back(blk.data());
         }
-        if (!fail && (fsm_single_unpad(L.u, S.dense, 1, L.nx, L.ny, L.nz, L.nxp, L.nyp, st) != hipSuccess ||
-                      hipMemcpyAsync(u, S.dense, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                      hipStreamSynchronize(st) != hipSuccess))
-            fail = 1;
         if (mceik_mpi_exchange_double(H.fcomm, (int)dir.size(), dir.data(), peer.data(), tag.data(), buf.data(),
                                       cnt.data()))
             fail = 1;
-        for (int r = 1; r < H.nranks && !fail; r++) {
-            const BlockBox &B = box[r];
-            size_t i = 0;
-            for (int z = 0; z < B.ext[2]; z++)
-                for (int y = 0; y < B.ext[1]; y++) {
-                    memcpy(u + ((size_t)(B.lo[2] + z) * L.ny + B.lo[1] + y) * L.nx + B.lo[0], &got[r][i],
-                           (size_t)B.ext[0] * 8);
-                    i += B.ext[0];
-                }
+        if (master && !fail) {
+            if (!blk.empty()) host_box(u, H.gn, own, blk.data(), false);
+            for (int r = 1; r < H.nranks; r++)
+                if (!got[r].empty()) host_box(u, H.gn, box[r], got[r].data(), false);
         }
-    } else if (mine.off[1]) {
-        std::vector<double> out(mine.off[1]);
-        if (fsm_box_copy(L, mine, S.dense, 1, st) != hipSuccess ||
-            hipMemcpyAsync(out.data(), S.dense, out.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            fail = 1;
-        int dir = 0, peer = 0, tag = 99, cnt = (int)out.size();
-        double *b = out.data();
-        if (mceik_mpi_exchange_double(H.fcomm, 1, &dir, &peer, &tag, &b, &cnt)) fail = 1;
     }
     if (mceik_mpi_allreduce_int(H.fcomm, &fail, 1, 1) || fail) return -1;
     return ierr;
@@ -1064,24 +1126,29 @@ extern "C" void eikonal3d_initialize(const int *comm, const int *iverb, const in
     if (e && rank <= 0) printf(" eikonal3d_initialize: Error computing local domain\n");
     const bool ranks = !e && rank >= 0 && nranks > 1 && nranks == nd[0] * nd[1] * nd[2];
     halo_free(g_halo);
-    if (!e && (rank <= 0 || ranks)) {            // the grid on the master's GPU, or on every rank's
+    if (ranks) {                                 // every rank holds its block and the ghost layer
+        if (halo_setup(g_halo, D, nn, *comm, rank, nranks)) {
+            if (rank == 0) printf(" eikonal3d_initialize: Error making the ghost communication structure\n");
+            e = 1;
+        } else {
+            if (rank_alloc(S, g_halo, ip[8], 1)) e = 2;
+            S.D = D;
+            if (!e && blocks_buffers(S)) e = 2;
+        }
+    } else if (!e && rank <= 0) {                // the grid on the master's GPU
         if (single_alloc(S, 1, nn[0], nn[1], nn[2], ip[8], 1)) e = 2;
         S.D = D;
         if (!e && (nd[0] * nd[1] * nd[2] > 1) && blocks_buffers(S)) e = 2;
-        if (e == 2) printf(" eikonal3d_initialize: Error making the device structures on process %d\n",
-                           rank > 0 ? rank : 0);
     }
+    if (e == 2) printf(" eikonal3d_initialize: Error making the device structures on process %d\n", rank > 0 ? rank : 0);
     // a failure on any rank's device is every rank's failure
     if (rank >= 0 && mceik_mpi_allreduce_int(*comm, &e, 1, 1)) e = 1;
-    if (!e && ranks && halo_setup(g_halo, D, nn, *comm, rank, nranks)) {
-        if (rank == 0) printf(" eikonal3d_initialize: Error making the ghost communication structure\n");
-        e = 1;
-    }
     if (e) {
+        halo_free(g_halo);
         *ierr = 1;
         return;
     }
-    S.nx = nn[0]; S.ny = nn[1]; S.nz = nn[2];
+    if (!ranks) { S.nx = nn[0]; S.ny = nn[1]; S.nz = nn[2]; }   // (ranks: S.n* are the box's, g_halo.gn the grid's)
     S.iverb = ip[0]; S.maxit = ip[8]; S.x0 = dp[0]; S.y0 = dp[1]; S.z0 = dp[2]; S.h = dp[3]; S.tol = dp[4];
     S.init = 1;
 }
@@ -1101,10 +1168,11 @@ extern "C" void eikonal3d_solve(const int *comm, const int *nsrc, const int *n, 
     const bool master = rank == 0 || (rank < 0 && (long)*n >= (long)S.nx * S.ny * S.nz);
     if (g_halo.on) {
         // the master's source count and argument check on every rank
+        const RankHalo &H = g_halo;
         int mp[2] = {*nsrc, 0};
-        if (master && (*nsrc < 1 || (long)*n < (long)S.nx * S.ny * S.nz)) mp[1] = 1;
+        if (master && (*nsrc < 1 || (long)*n < (long)H.gn[0] * H.gn[1] * H.gn[2])) mp[1] = 1;
         if (mceik_mpi_bcast_int(*comm, mp, 2, 0)) mp[1] = 1;
-        if (!mp[1] && single_alloc(S, 1, S.nx, S.ny, S.nz, S.maxit, mp[0])) mp[1] = 2;
+        if (!mp[1] && (rank_alloc(S, H, S.maxit, mp[0]) || blocks_buffers(S))) mp[1] = 2;
         if (mceik_mpi_allreduce_int(*comm, &mp[1], 1, 1)) mp[1] = 1;
         if (mp[1]) {
             if (master) printf(" eikonal3d_solve: Error setting bcs\n");

@@ -20,6 +20,10 @@ struct SingleLaunch {
     unsigned long long *arrive;      // [maxit] bricks done with the iteration | not-converged count << 32
     int *ierr_it;                    // [maxit] ierr of node (0,0,0) in the iteration's last sweep
     const int *bcerr;                // SETBCS failed (ierr = 1): no sweep runs
+    // The fields may hold a box of a larger grid (the MPI variant across ranks:
+    // a rank's block and its ghost layer): global dimensions and the global
+    // coordinates of local node 0.  The whole grid: g = n, o = 0.
+    int gx, gy, gz, ox, oy, oz;
 };
 
 // Block decomposition of the MPI variant (fsm3d.f90:1086-1101): nd blocks per

@@ -290,7 +290,7 @@ __global__ void single_setbcs_kernel(SingleLaunch L, const double *src, int nsrc
     for (int s = 0; s < nsrc && !bad; s++) {
         const double *sp = src + (size_t)s * 4;
         int loc[3][3];
-        const int nn[3] = {L.nx, L.ny, L.nz};
+        const int nn[3] = {L.gx, L.gy, L.gz};
         const double org[3] = {L.x0, L.y0, L.z0};
         for (int a = 0; a < 3; a++) {
             const double xs = sp[1 + a], x0 = org[a], dx = L.h;
@@ -315,12 +315,15 @@ __global__ void single_setbcs_kernel(SingleLaunch L, const double *src, int nsrc
         if (lane < 27) {
             const int i = lane % 3, j = (lane / 3) % 3, k = lane / 9;
             const int ix = loc[0][i], iy = loc[1][j], iz = loc[2][k];
-            if (ix != -1 && iy != -1 && iz != -1) {
+            // local node (the fields may hold a box of the grid: nodes outside it are skipped)
+            const int lx = ix - 1 - L.ox, ly = iy - 1 - L.oy, lz = iz - 1 - L.oz;
+            if (ix != -1 && iy != -1 && iz != -1 && lx >= 0 && lx < L.nx && ly >= 0 && ly < L.ny && lz >= 0 &&
+                lz < L.nz) {
                 const double x = L.x0 + (double)(ix - 1) * L.h, y = L.y0 + (double)(iy - 1) * L.h,
                              z = L.z0 + (double)(iz - 1) * L.h;
                 const double ddx = sp[1] - x, ddy = sp[2] - y, ddz = sp[3] - z;
                 const double dd = __builtin_sqrt((ddx * ddx + ddy * ddy) + ddz * ddz);
-                const size_t idx = (size_t)(iz - 1) * sz + (size_t)(iy - 1) * sy + (size_t)(ix - 1);
+                const size_t idx = (size_t)lz * sz + (size_t)ly * sy + (size_t)lx;
                 const R t = (R)(sp[0] + dd * (double)slow[idx]);
                 const R cur = u[idx];
                 u[idx] = (__builtin_fabs(dd) < 1.e-10) ? t : (cur < t ? cur : t);
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockD
 {
     const int b = blockIdx.x + b0;
     const int bi[3] = {b % D.nd[0], (b / D.nd[0]) % D.nd[1], b / (D.nd[0] * D.nd[1])};
-    const int nn[3] = {L.nx, L.ny, L.nz};
+    const int nn[3] = {L.gx, L.gy, L.gz};
     int lo[3], ext[3];
     for (int a = 0; a < 3; a++) {
         lo[a] = D.step[a] * bi[a];
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockD
             const int k3[3] = {kx, ky, kz};
             int c[3];
             for (int a = 0; a < 3; a++) c[a] = rev[a] ? lo[a] + ext[a] - 1 - k3[a] : lo[a] + k3[a];
-            const size_t idx = (size_t)c[2] * sz + (size_t)c[1] * sy + (size_t)c[0];
+            const size_t idx = (size_t)(c[2] - L.oz) * sz + (size_t)(c[1] - L.oy) * sy + (size_t)(c[0] - L.ox);
             if (L.bc[idx]) continue;                   // lupd = .FALSE. (SETBCS node)
             const double self = u[idx];
             double nb[6];
@@ -418,8 +421,8 @@ __global__ __launch_bounds__(256) void block_sweep_kernel(SingleLaunch L, BlockD
     }
 }
 
-// nodes of the box with !(|u0 - u| < tol) (the FSM_MPI convergence count,
-// fsm3d.f90:195-205; the whole grid, or the nodes a rank owns)
+// nodes of the box (global coordinates) with !(|u0 - u| < tol) (the FSM_MPI
+// convergence count, fsm3d.f90:195-205; the whole grid, or the nodes a rank owns)
 __global__ void block_unconverged_kernel(SingleLaunch L, BlockBox B, double tol, unsigned *count)
 {
     const size_t n = (size_t)B.ext[0] * B.ext[1] * B.ext[2];
@@ -428,15 +431,15 @@ __global__ void block_unconverged_kernel(SingleLaunch L, BlockBox B, double tol,
         const int x = B.lo[0] + (int)(i % B.ext[0]);
         const size_t t = i / B.ext[0];
         const int y = B.lo[1] + (int)(t % B.ext[1]), z = B.lo[2] + (int)(t / B.ext[1]);
-        const size_t p = ((size_t)z * L.nyp + y) * L.nxp + x;
+        const size_t p = ((size_t)(z - L.oz) * L.nyp + (y - L.oy)) * L.nxp + (x - L.ox);
         const double d = ((const double *)L.u0)[p] - ((const double *)L.u)[p];
         c += !(__builtin_fabs(d) < tol);
     }
     if (c) atomicAdd(count, c);
 }
 
-// Boxes of the padded fp64 grid <-> one contiguous buffer, box k at off[k],
-// x fastest inside a box: the halo faces a rank swaps after every sweep
+// Boxes of the padded fp64 grid (global coordinates, inside the fields' box)
+// <-> one contiguous buffer, box k at off[k], x fastest inside a box: the halo faces a rank swaps after every sweep
 // (EIKONAL_EXCHANGE, fsm3d.f90:971-1046) and the owned block it sends to the
 // master at the end (EIKONAL_GATHER_TRAVELTIMES).
 __global__ void box_copy_kernel(SingleLaunch L, BoxList bl, double *buf, int to_buf)
@@ -451,7 +454,7 @@ __global__ void box_copy_kernel(SingleLaunch L, BoxList bl, double *buf, int to_
         const int x = B.lo[0] + (int)(j % B.ext[0]);
         const size_t t = j / B.ext[0];
         const int y = B.lo[1] + (int)(t % B.ext[1]), z = B.lo[2] + (int)(t / B.ext[1]);
-        const size_t p = ((size_t)z * L.nyp + y) * L.nxp + x;
+        const size_t p = ((size_t)(z - L.oz) * L.nyp + (y - L.oy)) * L.nxp + (x - L.ox);
         if (to_buf) buf[i] = u[p];
         else u[p] = buf[i];
     }
