@@ -14,6 +14,7 @@
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <stddef.h>
+#include <stdlib.h>
 
 #define MCEIK_HIDDEN __attribute__((visibility("hidden")))
 
@@ -132,9 +133,9 @@ MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, 
 {
     if (!load()) return -1;
     if (nmsg <= 0) return 0;
-    if (nmsg > 64) return -1;
     MPI_Comm c = MPI_Comm_f2c((MPI_Fint)fcomm);
-    MPI_Request req[64];
+    MPI_Request rq[64], *req = nmsg <= 64 ? rq : (MPI_Request *)malloc(sizeof(MPI_Request) * (size_t)nmsg);
+    if (!req) return -1;
     int bad = 0;
     for (int k = 0; k < nmsg; k++) {
         const int r = dir[k] ? rt.irecv(buf[k], count[k], MPI_DOUBLE, peer[k], tag[k], c, &req[k])
@@ -142,6 +143,7 @@ MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, 
         if (r != MPI_SUCCESS) { req[k] = MPI_REQUEST_NULL; bad = 1; }
     }
     if (rt.waitall(nmsg, req, MPI_STATUSES_IGNORE) != MPI_SUCCESS) bad = 1;
+    if (req != rq) free(req);
     return bad ? -1 : 0;
 }
 #else
