@@ -70,6 +70,9 @@ __device__ __forceinline__ double godunov(double a, double b, double c, double f
 #ifndef MCEIK_F64_SELECT
 #define MCEIK_F64_SELECT 1
 #endif
+#ifndef MCEIK_F64_ONE_SQRT
+#define MCEIK_F64_ONE_SQRT 0     // 1: one square root per node (bitwise; measured 13% slower, profiles/r03_f64one)
+#endif
 __device__ __forceinline__ double godunov_sel(double a, double b, double c, double f, int &ierr)
 {
     const double UN = DBL_MAX;
@@ -79,6 +82,40 @@ __device__ __forceinline__ double godunov_sel(double a, double b, double c, doub
     const double x1 = a1 + f;
     const double amb = a1 - a2;
     const double arg = (2.0 * f) * f - amb * amb;
+#if MCEIK_F64_ONE_SQRT
+    // One square root per node.  The reference takes the 3D root when the 2D
+    // value x2 = 0.5*((a1 + a2) + sqrt(arg)) exceeds a3 (|a1 - a2| < f), i.e.
+    // when sqrt(arg) > T = 2*a3 - (a1 + a2).  Outside a band of half-width
+    // E = 2^-40 * (a1 + a2 + 2*a3 + 2*f) around T -- 2^11 times the rounding
+    // of every quantity involved (all of them are sums of a1..a3, f and
+    // sqrt(arg) <= sqrt(2) f) -- comparing arg with (T +- E)^2 gives the
+    // reference's decision on its rounded x2, so only the chosen radicand is
+    // square-rooted.  Inside the band (and for non-finite T or E) the lane
+    // decides on the literal x2.  Values and ierr identical to godunov().
+    const bool use2 = __builtin_fabs(amb) < f;
+    const double S = a1 + a2;
+    const double x2b = (a1 < a2 ? a1 : a2) + f;
+    const double T = 2.0 * a3 - S;
+    const double E = 0x1p-40 * ((S + 2.0 * a3) + 2.0 * f);
+    const double tp = T + E, tm = T - E;
+    const bool fin = E < 0x1p400;                           // T, E and their squares are finite
+    const bool open3 = a3 == UN;                            // x2 is finite: never above DBL_MAX
+    const bool sure3 = fin && !open3 && (tp < 0.0 || arg > tp * tp);   // sqrt(arg) > T + E: x2 > a3
+    const bool sure2 = open3 || (fin && tm > 0.0 && arg < tm * tm);    // sqrt(arg) < T - E: x2 < a3
+    const bool r1 = !(x1 > a2), nan_in = a1 == UN;
+    bool d3 = use2 ? sure3 : x2b > a3;                      // the reference's 3D case
+    if (use2 && !(sure3 || sure2)) d3 = 0.5 * (S + __builtin_sqrt(arg)) > a3;   // the band: its literal test
+    const double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
+    const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
+    const double disc = qb * qb - 4.0 * qc;
+    const double sq = __builtin_sqrt(d3 ? disc : arg);
+    const double x2 = use2 ? 0.5 * (S + sq) : x2b;
+    const double x3 = 0.5 * (-qb + sq);
+    const bool in3 = x3 < UN;
+    const int e3 = in3 ? (x3 < 0.0 ? 2 : (disc < 0.0 ? 1 : 0)) : 3;
+    ierr = (nan_in || r1 || !d3) ? 0 : e3;
+    return nan_in ? UN : r1 ? x1 : !d3 ? x2 : (in3 ? x3 : UN);
+#else
     const double x2 = __builtin_fabs(amb) < f ? 0.5 * ((a1 + a2) + __builtin_sqrt(arg)) : (a1 < a2 ? a1 : a2) + f;
     const double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
     const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
@@ -89,6 +126,7 @@ __device__ __forceinline__ double godunov_sel(double a, double b, double c, doub
     const int e3 = in3 ? (x3 < 0.0 ? 2 : (disc < 0.0 ? 1 : 0)) : 3;
     ierr = (nan_in || r1 || r2) ? 0 : e3;
     return nan_in ? UN : r1 ? x1 : r2 ? x2 : (in3 ? x3 : UN);
+#endif
 }
 
 // Correctly rounded sqrt for normal positive x (LLVM's expansion without the
