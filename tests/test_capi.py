@@ -143,3 +143,24 @@ def test_ctypes_batch_structs_match_public_headers(header, ctype, pyname):
     assert C.sizeof(cls) == c["sizeof"]
     for n in names:
         assert getattr(cls, n).offset == c[n], n
+
+
+@pytest.mark.parametrize("src,mpi", [("xfsm3d_gpu.c", False), ("mcmc_main.c", False), ("xfsm3d_mpi.c", True),
+                                     ("mpi_sampler_main.c", True), ("blocks_mpi_gpu.c", True)])
+def test_c_callers_compile_and_link(tmp_path, src, mpi):
+    """The C callers the GPU tests run (tests/c/*.c) build against include/ and
+    link against libmceik_hip.so here on the CPU, so a header or ABI drift
+    shows without a GPU (MPI callers against the image's MPICH)."""
+    lib = os.path.join(ROOT, "mceik_amd")
+    mpidir = "/opt/conda"
+    if mpi and not (os.path.exists(f"{mpidir}/include/mpi.h") and os.path.exists(f"{mpidir}/lib/libmpi.so")):
+        pytest.skip("no MPI toolchain in this image")
+    cmd = ["gcc", "-O1", "-I", os.path.join(ROOT, "include")]
+    if mpi:
+        cmd += ["-I", f"{mpidir}/include"]
+    cmd += [os.path.join(ROOT, "tests", "c", src), "-L", lib, "-lmceik_hip"]
+    if mpi:
+        cmd += [f"{mpidir}/lib/libmpi.so"]
+    cmd += [f"-Wl,-rpath,/usr/lib/x86_64-linux-gnu:{lib}" + (f":{mpidir}/lib" if mpi else ""), "-lm",
+            "-o", str(tmp_path / "caller")]
+    subprocess.run(cmd, check=True)
