@@ -121,6 +121,107 @@ def cpu_baseline(p, v0, cores, rounds=CPU_ROUNDS):
                       f"{float(np.max(times)):.3f} s; proposals/s = cores / median / {p.nstat} stations"}
 
 
+# ---------------------------------------------------------------- roofline
+def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config):
+    """The `roofline` object of a timed region: algorithmic bytes of the FSM
+    launches (visited bricks x nodes x bytes per node sweep)
+    over the FSM time of a step -- the HIP-event launch duration with one
+    pipe, the wall time per step with overlapped pipes."""
+    fsm_ms, nlaunch, iters, (bricks, segs, segs_changed, wsteps) = stats
+    n_nodes = p.nx * p.ny * p.nz
+    from mceik_amd import _lib
+    b = _lib.FsmBatch(); b.precision = precision; b.slow_mode = 1; b.nstat = p.nstat
+    b.nrx, b.nry, b.nrz = p.nref
+    bpn = _lib.lib().mceik_fsm_bytes_per_node_sweep(C.byref(b))
+    # the instance the sampler launches (same batch geometry as mceik_mcmc_init)
+    b.nx, b.ny, b.nz, b.h = p.nx, p.ny, p.nz, p.h
+    b.nmodel, b.nsrc, b.fast_sqrt, b.maxit, b.tol = per_gpu, 1, int(precision == 32), p.maxit, p.tol
+    b.nev = p.nevents
+    step_z = _lib.lib().mceik_fsm_step_z(C.byref(b))
+    kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
+             "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)"
+             if precision == 32 else "fsm_solve_kernel<double, 2, false, 2, 1, 4> (8-z steps, fp64 literal update)")
+    # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
+    # inputs did not change since their last visit are skipped, DESIGN.md s.3.1)
+    nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
+    alg_bytes = bricks * (n_nodes / nbricks) * bpn    # this rank's launches
+    full_bytes = iters * 8.0 * n_nodes * bpn          # the same iterations without skipping
+    avg_ms = fsm_ms / max(nlaunch, 1)
+    steps = max(nsteps, 1)
+    solves_per_step = per_gpu * p.nstat                 # this rank's (chain, station) solves
+    alg_step = alg_bytes / steps                        # algorithmic bytes of one step (all pipes)
+    achieved = per_launch = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
+    pipes = round(nlaunch / steps)                      # 1 if the sampler fell back to one pipe
+    if pipes > 1:
+        # two half launches per step, overlapped: a half's HIP-event span also
+        # covers the time it waits for the other half's waves, so price one
+        # step's algorithmic bytes on the step's wall time instead (includes
+        # propose/accept and the gather: conservative)
+        achieved = alg_bytes / elapsed / 1e9                  # this rank's bytes, the timed region
+    # the FSM time of one step: the single launch (HIP events) or, with pipes,
+    # the wall time per step (the overlapped half launches' union is shorter)
+    step_fsm_s = avg_ms * 1e-3 if pipes <= 1 else elapsed / steps
+    traffic = traffic_src = None
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            tj = json.load(f)
+        rec = tj.get("f64", {}) if precision == 64 else tj
+        if (rec.get("workload") == config and rec.get("chains_per_gpu") == per_gpu
+                and rec.get("kernel_rev") == KERNEL_REV):
+            traffic = rec.get("hbm_bytes_per_launch")     # one single-pipe launch = one step
+            traffic_src = (f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of kernel_rev {KERNEL_REV} "
+                           f"({rec.get('source', 'profiles/traffic.json')}); not measured in this run")
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": kname,
+            "kernel_rev": KERNEL_REV,
+            "timing": (f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
+                       if pipes > 1 else "HIP events around each FSM launch"),
+            "per": "step: every per-unit field below is per step or per solve, whatever the pipes",
+            "pipes": pipes,
+            "alg_bytes_per_step": alg_step,
+            "traffic_per_step": traffic, "traffic_source": traffic_src,
+            "traffic_over_alg": round(traffic / alg_step, 4) if traffic else None,
+            "bytes_per_node_sweep": bpn,
+            "fsm_s_per_step": round(step_fsm_s, 4),
+            "launches_per_step": round(nlaunch / steps, 3), "avg_launch_ms": round(avg_ms, 3),
+            "frac_per_launch_events": round(per_launch / HBM_PEAK_GBS, 4),
+            "solves_per_step": solves_per_step,
+            "iterations_per_solve": round(iters / steps / solves_per_step, 3),
+            "brick_visit_fraction": round(bricks / max(1.0, iters * 8.0 * nbricks), 4),
+            "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),
+            "wave_steps_per_step": wsteps / steps,
+            "full_sweep_equiv_GBs": round(full_bytes / steps / step_fsm_s / 1e9, 1)}
+
+
+def f64_record(p, v0, per_gpu, args, dev, stream):
+    """The reference's own precision on the same workload, after the f32 timed
+    region: a --precision 64 sampler (the literal fp64 update, fsm3d.f90:624-693)
+    of the same chains, `f64_warmup` untimed + `f64_steps` timed steps bracketed
+    like the headline's, with its own roofline.  One GPU only."""
+    import torch
+    from mceik_amd import mcmc
+    torch.cuda.empty_cache()
+    smp = mcmc.Sampler(p, nchains=per_gpu, chain_offset=0, v0=v0, max_samples=1, device=dev.index, precision=64)
+    smp.set_stream(stream.cuda_stream)
+    if args.f64_warmup:
+        smp.run(args.f64_warmup)
+    smp.fsm_stats(reset=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    smp.run(args.f64_steps)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    stats = smp.fsm_stats()
+    smp.close()
+    return {"value": round(per_gpu * args.f64_steps / elapsed, 3), "unit": "proposals/s", "dtype": "f64",
+            "steps": args.f64_steps, "warmup": args.f64_warmup,
+            "ms_per_step": round(elapsed / args.f64_steps * 1e3, 2),
+            "roofline": roofline(p, per_gpu, 64, stats, elapsed, args.f64_steps, args.config)}
+
+
+
 # ---------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -136,6 +237,9 @@ def main():
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64),
                     help="FSM arithmetic (64: the reference's literal fp64 update; tables fp32 either way)")
+    ap.add_argument("--f64-steps", type=int, default=2,
+                    help="timed steps of the appended fp64 record (one GPU, --precision 32 runs; 0 = none)")
+    ap.add_argument("--f64-warmup", type=int, default=1)
     ap.add_argument("--pipes", type=int, default=2, choices=(1, 2, 3, 4),
                     help="the sampler's chains as two halves on two streams (the library default, DESIGN.md "
                          "s.3.5) or one launch per step (1)")
@@ -228,6 +332,10 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     smp.run(args.steps)
+    # this rank's steps end here (the gather waits for them anyway): the split
+    # attributes an N > 1 efficiency loss to the step spread or the gather
+    torch.cuda.synchronize(dev)
+    t_steps = time.perf_counter()
     # checkpoint: the kept posterior states of every chain -> rank 0 (RCCL over xGMI)
     if world > 1 and comm is not None:
         comm.gather(smp, per_gpu * world, which=1, root=0, v_out=post, logl_out=post_l if rank == 0 else None)
@@ -239,14 +347,20 @@ def main():
     else:
         smp.samples(max_states=1, device_ptr=post.data_ptr())
     torch.cuda.synchronize(dev)
+    t_gather = time.perf_counter()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    per_rank = [[t_steps - t0, t_gather - t_steps]]            # [steps s, gather s] of each rank
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        mine = torch.tensor(per_rank[0], dtype=torch.float64, device=red_dev)
+        every = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        per_rank = [e.tolist() for e in every]
     gather_check = None
     if world > 1 and comm is not None:
         # outside the timed region: the library gather == torch.distributed's gather
@@ -255,55 +369,16 @@ def main():
             gather_check = bool(torch.equal(tv.to(dev), post) and torch.equal(tl.to(dev), post_l))
         if comm is not None:
             comm.close()
-    fsm_ms, nlaunch, iters, (bricks, segs, segs_changed, wsteps) = smp.fsm_stats()
+    stats = smp.fsm_stats()
     _, logl, nacc, _ = smp.state()
     smp.close()
+    f64 = None
+    if world == 1 and args.precision == 32 and args.f64_steps > 0:
+        f64 = f64_record(p, v0, per_gpu, args, dev, stream)
 
     if rank == 0:
-        n_nodes = p.nx * p.ny * p.nz
         total = per_gpu * world * args.steps
-        from mceik_amd import _lib
-        b = _lib.FsmBatch(); b.precision = args.precision; b.slow_mode = 1; b.nstat = p.nstat
-        b.nrx, b.nry, b.nrz = p.nref
-        bpn = _lib.lib().mceik_fsm_bytes_per_node_sweep(C.byref(b))
-        # the instance the sampler launches (same batch geometry as mceik_mcmc_init)
-        b.nx, b.ny, b.nz, b.h = p.nx, p.ny, p.nz, p.h
-        b.nmodel, b.nsrc, b.fast_sqrt, b.maxit, b.tol = per_gpu, 1, int(args.precision == 32), p.maxit, p.tol
-        b.nev = p.nevents
-        step_z = _lib.lib().mceik_fsm_step_z(C.byref(b))
-        kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
-                 "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)"
-                 if args.precision == 32 else "fsm_solve_kernel<double, ...> (8-z steps, fp64 literal update)")
-        # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
-        # inputs did not change since their last visit are skipped)
-        nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
-        alg_bytes = bricks * (n_nodes / nbricks) * bpn    # this rank's launches
-        full_bytes = iters * 8.0 * n_nodes * bpn          # the same iterations without skipping
-        avg_ms = fsm_ms / max(nlaunch, 1)
-        steps = max(args.steps, 1)
-        solves_per_step = per_gpu * p.nstat                 # this rank's (chain, station) solves
-        alg_step = alg_bytes / steps                        # algorithmic bytes of one step (all pipes)
-        achieved = per_launch = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
-        pipes = round(nlaunch / steps)                      # 1 if the sampler fell back to one pipe
-        if pipes > 1:
-            # two half launches per step, overlapped: a half's HIP-event span also
-            # covers the time it waits for the other half's waves, so price one
-            # step's algorithmic bytes on the step's wall time instead (includes
-            # propose/accept and the gather: conservative)
-            achieved = alg_bytes / elapsed / 1e9                  # this rank's bytes, the timed region
-        # the FSM time of one step: the single launch (HIP events) or, with pipes,
-        # the wall time per step (the overlapped half launches' union is shorter)
-        step_fsm_s = avg_ms * 1e-3 if pipes <= 1 else elapsed / steps
-        traffic = traffic_src = None
-        tf = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                tj = json.load(f)
-            if (tj.get("workload") == args.config and tj.get("chains_per_gpu") == per_gpu
-                    and tj.get("kernel_rev") == KERNEL_REV and args.precision == 32):
-                traffic = tj.get("hbm_bytes_per_launch")      # one single-pipe launch = one step
-                traffic_src = (f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of kernel_rev {KERNEL_REV} "
-                               f"({tj.get('source', 'profiles/traffic.json')}); not measured in this run")
+        rl = roofline(p, per_gpu, args.precision, stats, elapsed, args.steps, args.config)
         line = {
             "metric": METRIC,
             "value": round(total / elapsed, 3),
@@ -322,41 +397,28 @@ def main():
                                    f"{p.nevents} events, nref=4",
                        "chains_per_gpu": per_gpu, "chains_total": per_gpu * world, "grid": [p.nx, p.ny, p.nz],
                        "stations": p.nstat, "events": p.nevents, "parallelism": f"chains sharded over {world} GPU(s)",
-                       "pipes": pipes},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": kname,
-                         "kernel_rev": KERNEL_REV,
-                         "timing": (f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
-                                    if pipes > 1 else "HIP events around each FSM launch"),
-                         "per": "step: every per-unit field below is per step or per solve, whatever the pipes",
-                         "alg_bytes_per_step": alg_step,
-                         "traffic_per_step": traffic, "traffic_source": traffic_src,
-                         "traffic_over_alg": round(traffic / alg_step, 4) if traffic else None,
-                         "bytes_per_node_sweep": bpn,
-                         "fsm_s_per_step": round(step_fsm_s, 4),
-                         "launches_per_step": round(nlaunch / steps, 3), "avg_launch_ms": round(avg_ms, 3),
-                         "frac_per_launch_events": round(per_launch / HBM_PEAK_GBS, 4),
-                         "solves_per_step": solves_per_step,
-                         "iterations_per_solve": round(iters / steps / solves_per_step, 3),
-                         "brick_visit_fraction": round(bricks / max(1.0, iters * 8.0 * nbricks), 4),
-                         "changed_segment_fraction": round(segs_changed / max(1.0, segs), 4),
-                         "wave_steps_per_step": wsteps / steps,
-                         "full_sweep_equiv_GBs": round(full_bytes / steps / step_fsm_s / 1e9, 1)},
+                       "pipes": rl["pipes"]},
+            "roofline": rl,
             "cpu_baseline": cpu,
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
         if rehearse:
             line["ranks"] = world
             line["rehearsal"] = "one GPU shared by all ranks (MCEIK_BENCH_REHEARSAL=1): not a scaling measurement"
+        st = [r[0] / args.steps * 1e3 for r in per_rank]
+        line["rank_step_ms"] = {"min": round(min(st), 2), "max": round(max(st), 2), "ranks": len(st)}
+        line["gather_ms"] = round(max(r[1] for r in per_rank) * 1e3, 3)
         if world > 1:
             line["gather"] = {"path": gather_path}
             if gather_check is not None:
                 # the library's RCCL gather checked against torch.distributed's (outside the timed region)
                 line["gather"]["equals_torch_gather"] = gather_check
         if args.raw_stats:
-            line["fsm_raw"] = {"bricks": bricks, "segs": segs, "segs_changed": segs_changed, "iters": iters,
-                               "wave_steps": wsteps, "launches": nlaunch}
+            ms, nl, it, (br, sg, sgc, ws) = stats
+            line["fsm_raw"] = {"bricks": br, "segs": sg, "segs_changed": sgc, "iters": it, "wave_steps": ws,
+                               "launches": nl}
+        if f64 is not None:
+            line["f64"] = f64
         if cpu:
             line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         print(json.dumps(line), flush=True)

@@ -92,9 +92,15 @@ int mceik_parms_write(const char *path, const struct mceik_parms_struct *parms, 
 
 /* v0: host [nchains][nphase][ncell] int m/s (P model, then S model when
  * nphase = 2), ncell = ceil(nx/nrefx)*ceil(ny/nrefy)*ceil(nz/nrefz), cell
- * index x fastest.  Computes each chain's initial logL.  Returns 1 on invalid
- * arguments (and on used S picks with nphase 1 unless mask_s), 2 when a
- * station's solve fails (the reference's ierr), -1 on a device failure.
+ * index x fastest.  Computes each chain's initial logL.  Stations need
+ * Cartesian coordinates (lcartesian = 1); a station gets a P table only when
+ * lhasP[k] and an S table only when lhasS[k] is set (NULL arrays: every
+ * station), the other solves are skipped.  Returns 1 on invalid arguments
+ * (lcartesian != 1, a used pick at a station without its phase flag, used S
+ * picks with nphase 1 unless mask_s), 2 when a station's solve fails (the
+ * reference's ierr), -1 on a device failure.  A failed multi-step queue
+ * (mceik_mcmc_get_info multi_step) is reported as -1 by the next
+ * synchronising call (sync, get_state, get_samples, checkpoint).
  * Every array below sized [nchains][ncell] is [nchains][nphase][ncell]. */
 int mceik_mcmc_init(const struct mceik_parms_struct *parms,
                     const struct mceik_stations_struct *stations,
@@ -142,6 +148,10 @@ int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *logl, const lo
  * Synchronises. */
 int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nlaunch, unsigned long long *iters,
                          unsigned long long *visits, int reset);
+/* Solves executed since init (or the last fsm_stats reset): solves of a
+ * station without picks of the solve's phase are skipped (lhasP / lhasS,
+ * homog.c:313-335) and not counted.  Synchronises. */
+int mceik_mcmc_fsm_solves(mceik_mcmc *s, unsigned long long *solves);
 int mceik_mcmc_finalize(mceik_mcmc **s);
 
 /* ---- multi-rank runs (one process per GPU; csrc/comm.hip) ---------------

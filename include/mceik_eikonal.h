@@ -47,8 +47,8 @@ void eikonal3d_serial_driver_sp(const int *job, const int *iverb, const int *max
  * with one MPI rank per block; one block = the serial driver's solve.  With
  * as many ranks in comm as blocks (the reference's layout) every rank holds
  * only its block and the ghost layer on its GPU, sweeps the block and swaps
- * face layers with its neighbours after every sweep (RCCL when each rank has a GPU of its own, host-staged MPI when
- * ranks share one; MCEIK_HALO=mpi|rccl), and the master gathers u; otherwise
+ * face layers with its neighbours after every sweep (host-staged MPI; MCEIK_HALO=rccl moves them device to
+ * device over RCCL when each rank has a GPU of its own, unpinned), and the master gathers u; otherwise
  * the master's GPU runs every block.  The master passes the full arrays
  * (n = nx*ny*nz) and receives u; the other ranks pass n = 1 as the
  * reference's callers do and keep their u.  fp64 (xfsm3d: max u =
@@ -163,6 +163,12 @@ typedef struct mceik_fsm_batch {
                                    slowness slow[(m*nphase + model_phase[m])*ncell ...] -- one of the
                                    nphase models (P, S) a sampler chain holds; NULL: slow[m*ncell ...] */
     int nphase;                 /* models per entry of `slow` when model_phase != NULL (1 or 2) */
+    const unsigned char *skip;  /* device [nphase][nstat] or NULL: solve (m, s) of phase ph (model_phase[m];
+                                   without a phase map m % nphase, i.e. models [chain][phase]) is skipped when skip[ph*nstat + s] != 0 -- a
+                                   station with no picks of that phase (mceik_stations_struct lhasP /
+                                   lhasS; homog.c:313-335 builds tables only for flagged stations): no
+                                   sweep, niter 0, ierr 0, its ttab row FLT_MAX (the unreached value) */
+    unsigned long long *solve_count; /* device counter += solves executed (not skipped), or NULL */
 } mceik_fsm_batch;
 
 /* The batched extension of SURVEY s.8b with plain arguments: nmodels x

@@ -25,7 +25,8 @@ class FsmBatch(C.Structure):
                 ("max_sweeps", C.c_int), ("iter_total", C.c_void_p), ("fast_sqrt", C.c_int),
                 ("visit_stats", C.c_void_p), ("solve_order", C.c_void_p), ("solve_clock", C.c_void_p),
                 ("max_waves", C.c_int), ("traffic", C.c_void_p), ("step_z", C.c_int),
-                ("ev_frac", C.c_void_p), ("model_phase", C.c_void_p), ("nphase", C.c_int)]
+                ("ev_frac", C.c_void_p), ("model_phase", C.c_void_p), ("nphase", C.c_int),
+                ("skip", C.c_void_p), ("solve_count", C.c_void_p)]
 
 
 class RelocateBatch(C.Structure):
@@ -96,7 +97,7 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_b
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
            "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize", "mceik_mcmc_last_phase",
-           "mceik_mcmc_get_info",
+           "mceik_mcmc_get_info", "mceik_mcmc_fsm_solves",
            "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write",
            "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather",
            "os_path_exists", "os_path_isdir", "os_path_isfile", "os_makedirs", "os_mkdir")
@@ -166,6 +167,8 @@ def lib():
     L.mceik_mcmc_fsm_stats.restype = C.c_int
     L.mceik_mcmc_fsm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong),
                                        C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]
+    L.mceik_mcmc_fsm_solves.restype = C.c_int
+    L.mceik_mcmc_fsm_solves.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     L.mceik_comm_unique_id.restype = C.c_int
     L.mceik_comm_unique_id.argtypes = [C.c_void_p]
     L.mceik_comm_init.restype = C.c_int

@@ -97,6 +97,8 @@ static void fill_launch(FsmLaunch &L, const mceik_fsm_batch *b)
     L.magic_rz = ((1u << 20) + L.nrz - 1) / L.nrz;
     L.ev_node = b->ev_node; L.nev = b->nev; L.ttab = b->ttab; L.ev_frac = b->ev_frac;
     L.model_phase = b->slow_mode == 1 ? b->model_phase : nullptr;
+    L.skip = b->skip;
+    L.solve_count = b->solve_count;
     L.nphase = b->nphase > 0 ? b->nphase : 1;
     // LDS cell cache when every z-block's cells fit (2 x 2 x 8 at nref = 4, kb = 4)
     {
@@ -256,7 +258,8 @@ extern "C" double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b)
 #define MCEIK_MC_CHUNK 64        // steps per multi-step launch (bounds one kernel's duration)
 struct McmcExt {
     const void *dev;             // device copy of the sampler's McmcDev
-    unsigned *sync;              // MC_SYNC_WORDS(nchains) words, zeroed here before the launch
+    unsigned *sync;              // MC_SYNC_WORDS(nchains) words, zeroed here before the launch (but the last)
+    unsigned spin_limit;
     int step0, nsteps, nburn, keepk, maxs, nkept0;
 };
 
@@ -321,9 +324,11 @@ static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_
         if (is_double || fsm_launch_kind(L, 0) != 16 || b->solve_order || b->u_out) return 1;
         L.mc_dev = ext->dev;
         L.mc_sync = ext->sync;
+        L.mc_spin_limit = ext->spin_limit;
         L.mc_step0 = ext->step0; L.mc_nsteps = ext->nsteps;
         L.mc_nburn = ext->nburn; L.mc_keepk = ext->keepk; L.mc_maxs = ext->maxs; L.mc_nkept0 = ext->nkept0;
-        HIPCHK(fsm_zero_words(ext->sync, MC_SYNC_WORDS(L.nsolve / L.nstat), st));
+        // the broken-queue flag (last word) persists until the sampler reports it
+        HIPCHK(fsm_zero_words(ext->sync, MC_SYNC_WORDS(L.nsolve / L.nstat) - 1, st));
     }
     HIPCHK(fsm_launch(L, is_double, w.nwaves, st));
     if (b->u_out) {
@@ -735,7 +740,7 @@ extern "C" int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, co
 // the one-GPU block kernel restricted to block b0 with the ghost snapshot
 // being u itself.  Transport of the face layers: RCCL device to device when
 // every rank has a GPU of its own (xGMI), host-staged MPI when ranks share a
-// GPU (RCCL takes one rank per GPU); MCEIK_HALO=mpi|rccl overrides.
+// GPU (RCCL takes one rank per GPU).  Default MPI; MCEIK_HALO=rccl|auto opts in.
 struct RankHalo {
     int on;                      // the solve runs one block per rank
     int fcomm, rank, nranks;
@@ -855,9 +860,13 @@ static int halo_setup(RankHalo &H, const BlockDecomp &D, const int nn[3], int fc
         (hipMalloc(&H.d_buf, (nsend + nrecv) * 8) != hipSuccess ||
          hipHostMalloc(&H.h_buf, (nsend + nrecv) * 8, hipHostMallocDefault) != hipSuccess))
         e = 1;
-    // transport: RCCL only when no two ranks share a GPU
+    // transport: host-staged MPI by default (the transport the bitwise
+    // across-ranks tests pin); MCEIK_HALO=rccl forces RCCL device to device,
+    // MCEIK_HALO=auto picks RCCL when no two ranks share a GPU.  The RCCL face
+    // swap needs one GPU per rank, which this build's test pool never had, so
+    // its parity is unpinned and it stays opt-in.
     const char *env = getenv("MCEIK_HALO");
-    int want = env && !strcmp(env, "mpi") ? 1 : env && !strcmp(env, "rccl") ? 2 : 0;
+    int want = env && !strcmp(env, "rccl") ? 2 : env && !strcmp(env, "auto") ? 0 : 1;
     if (!want) {
         char id[128] = {0};
         int dev = 0;
@@ -1034,8 +1043,11 @@ static int blocks_solve_ranks(SingleState &S, RankHalo &H, int nsrc, const doubl
                       hipMemcpyAsync(&ierr, d_ierr, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                       hipStreamSynchronize(st) != hipSuccess))
             fail = 1;
-        int tot[2] = {(int)std::min<unsigned>(count, 1u << 30), fail};
-        if (mceik_mpi_allreduce_int(H.fcomm, tot, 2, 0)) return -1;
+        // the reference sums the unconverged counts (fsm3d.f90:198-211) and tests
+        // for zero: a max over "any left" flags is that test without the sum's
+        // overflow on large blocks
+        int tot[2] = {count ? 1 : 0, fail};
+        if (mceik_mpi_allreduce_int(H.fcomm, tot, 2, 1)) return -1;
         if (tot[1]) return -1;
         if (tot[0] == 0) break;
     }
@@ -1458,7 +1470,7 @@ extern "C" int mceik_relocate(const mceik_relocate_batch *b, void *stream)
 // MCMC sampler (include/mceik.h)
 #define MCEIK_EV_RING 32           // hipEvent pairs around timed FSM launches (fixed ring)
 #define MCEIK_MAX_PIPES 4
-#define MCEIK_ITERS_N (5 + MCEIK_TRAFFIC_N)   // d_iters: iterations, 4 visit statistics, traffic
+#define MCEIK_ITERS_N (6 + MCEIK_TRAFFIC_N)   // d_iters: iterations, 4 visit statistics, solves, traffic
 
 struct mceik_mcmc {
     McmcDev D;
@@ -1484,6 +1496,7 @@ struct mceik_mcmc {
     // (fsm16_kernel.hip mc_finish), so no step waits for the slowest chain of
     // the one before.  d_dev: device copy of D; d_sync: the launch's queues.
     bool persist;
+    unsigned spin_limit;               // multi-step launches: polls before a wait counts as a broken queue
     McmcDev *d_dev;
     unsigned *d_sync;
     hipStream_t pst[MCEIK_MAX_PIPES];
@@ -1818,6 +1831,33 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
             fprintf(stderr, "mceik_mcmc_init: observation %d has varObs <= 0\n", j);
             return 1;
         }
+    // station coordinates are metres on the grid (lcartesian = 1, as homog.c
+    // sets them); geographic station lists are not converted
+    if (st->lcartesian != 1) {
+        fprintf(stderr, "mceik_mcmc_init: stations.lcartesian = %d: only Cartesian station coordinates (metres, "
+                        "lcartesian = 1) are supported\n", st->lcartesian);
+        return 1;
+    }
+    // Tables only for the phases a station has picks of (lhasP / lhasS,
+    // mceik_struct.h:43-46; homog.c:313-335 builds exactly those): the other
+    // solves are skipped.  A fit pick at a station without its flag would
+    // read a table never made, so the catalog is refused.
+    std::vector<unsigned char> skip((size_t)nphase * nstat, 0);
+    for (int k = 0; k < nstat; k++) {
+        skip[k] = st->lhasP ? st->lhasP[k] == 0 : 0;
+        if (nphase == 2) skip[(size_t)nstat + k] = st->lhasS ? st->lhasS[k] == 0 : 0;
+    }
+    for (int j = 0; j < nobs; j++)
+        if (fit_obs(j)) {
+            const int k = cat->statPtr[j] - 1, sph = cat->pickType[j] == S_PRIMARY_PICK;
+            if (skip[(size_t)sph * nstat + k]) {
+                fprintf(stderr, "mceik_mcmc_init: observation %d is a used %s pick at station %d (1-based) whose "
+                                "%s = 0\n", j, sph ? "S" : "P", k + 1, sph ? "lhasS" : "lhasP");
+                return 1;
+            }
+        }
+    int nskip = 0;
+    for (unsigned char c : skip) nskip += c;
     DeviceScope dg(o->device);
     if (hipSetDevice(o->device) != hipSuccess) return -1;
     mceik_mcmc *s = new mceik_mcmc();
@@ -1894,6 +1934,8 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     rc |= dput(s, &d_tobs, (const double *)cat->tobs, (size_t)(nobs > 0 ? nobs : 0));
     rc |= dput(s, &d_tcorr, tcorr.data(), tcorr.size());
     rc |= dput(s, &d_var, (const double *)cat->varObs, (size_t)(nobs > 0 ? nobs : 0));
+    unsigned char *d_skip = nullptr;
+    if (nskip) rc |= dput(s, &d_skip, skip.data(), skip.size());
     rc |= dput(s, &D.v, v0, (size_t)nch * ncm);
     rc |= dput(s, &D.slow_cur, sl.data(), sl.size());
     rc |= dput(s, &D.slow_prop, sl.data(), sl.size());
@@ -1909,7 +1951,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     if (nphase > 1) rc |= dalloc(s, &D.ttab_cur, (size_t)nch * nphase * nstat * nev);
     rc |= dalloc(s, &d_niter, (size_t)nch * nphase * nstat);
     rc |= dalloc(s, &s->d_ierr, (size_t)nch * nphase * nstat);
-    rc |= dalloc(s, &s->d_iters, MCEIK_ITERS_N);       // [0] iterations, [1..4] visit_stats, [5..] traffic
+    rc |= dalloc(s, &s->d_iters, MCEIK_ITERS_N);       // [0] iterations, [1..4] visit_stats, [5] solves, [6..] traffic
     if (s->max_samples) {
         rc |= dalloc(s, &D.keep_v, (size_t)s->max_samples * nch * ncm);
         rc |= dalloc(s, &D.keep_logl, (size_t)s->max_samples * nch);
@@ -1934,7 +1976,9 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.max_sweeps = -1;
     b.iter_total = s->d_iters;
     b.visit_stats = s->d_iters + 1;
-    b.traffic = s->d_iters + 5;
+    b.solve_count = s->d_iters + 5;
+    b.traffic = s->d_iters + 6;
+    b.skip = d_skip;
     b.max_waves = o->max_waves > 0 ? o->max_waves : 0;
     // f = h/v stays a normal float: the short correctly rounded sqrt (fp32 only)
     const int vhi = nphase == 2 ? std::max(o->vmax, o->vsmax) : o->vmax;
@@ -2002,6 +2046,9 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
         mceik_mcmc_finalize(&s);
         return -1;
     }
+    // MCEIK_MC_SPIN_LIMIT (test hook): polls before a multi-step wait gives up
+    const char *spin_env = getenv("MCEIK_MC_SPIN_LIMIT");
+    s->spin_limit = spin_env ? (unsigned)strtoul(spin_env, nullptr, 10) : 1u << 24;
     const char *pipe_env = getenv("MCEIK_PIPES");       // default 2; MCEIK_PIPES=1: one pipe
     int np = s->persist ? 1 : pipe_env ? atoi(pipe_env) : 2;
     np = np < 1 ? 1 : np > MCEIK_MAX_PIPES ? MCEIK_MAX_PIPES : np;
@@ -2033,7 +2080,7 @@ static int mcmc_steps(mceik_mcmc *s, int nsteps)
         for (int done = 0; done < nsteps;) {
             const int n = std::min(nsteps - done, MCEIK_MC_CHUNK);
             McmcExt x;
-            x.dev = s->d_dev; x.sync = s->d_sync;
+            x.dev = s->d_dev; x.sync = s->d_sync; x.spin_limit = s->spin_limit;
             x.step0 = (int)s->step; x.nsteps = n;
             x.nburn = s->nburn; x.keepk = s->keepk; x.maxs = s->max_samples; x.nkept0 = s->nkept;
             HIPCHK(mcmc_propose(s->D, (uint64_t)s->step, s->stream));
@@ -2097,12 +2144,26 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
     return rc;
 }
 
+// After a stream synchronisation: a multi-step launch whose wave gave up
+// waiting for a chain's step (the broken-queue flag) failed, and the chains'
+// state is not to be trusted; every later synchronising call reports it.
+static int mc_queue_check(mceik_mcmc *s, const char *who)
+{
+    if (!s->persist) return 0;
+    unsigned flag = 0;
+    HIPCHK(hipMemcpy(&flag, s->d_sync + MC_SYNC_WORDS(s->D.nchains) - 1, sizeof(flag), hipMemcpyDeviceToHost));
+    if (!flag) return 0;
+    fprintf(stderr, "%s: a multi-step launch timed out waiting for a chain's previous step (broken work queue); "
+                    "the chain state is invalid\n", who);
+    return -1;
+}
+
 extern "C" int mceik_mcmc_sync(mceik_mcmc *s)
 {
     if (!s) return 1;
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
-    return 0;
+    return mc_queue_check(s, "mceik_mcmc_sync");
 }
 
 extern "C" int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long long *naccept, long long *step)
@@ -2110,6 +2171,7 @@ extern "C" int mceik_mcmc_get_state(mceik_mcmc *s, int *v, double *logl, long lo
     if (!s) return 1;
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
+    if (mc_queue_check(s, "mceik_mcmc_get_state")) return -1;
     const McmcDev &D = s->D;
     if (v) HIPCHK(hipMemcpy(v, D.v, (size_t)D.nchains * D.ncm * 4, hipMemcpyDeviceToHost));
     if (logl) HIPCHK(hipMemcpy(logl, D.logl, (size_t)D.nchains * 8, hipMemcpyDeviceToHost));
@@ -2177,6 +2239,7 @@ extern "C" int mceik_mcmc_get_samples(mceik_mcmc *s, void *v_out, double *logl_o
     if (n <= 0) return 0;
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
+    if (mc_queue_check(s, "mceik_mcmc_get_samples")) return -1;
     hipMemcpyKind k = kind ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     const size_t per = (size_t)s->D.nchains * s->D.ncm;
     // ring slot of the i-th of the n most recent states: (nkept - n + i) mod max_samples
@@ -2271,12 +2334,12 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
     HIPCHK(hipMemcpy(it, s->d_iters, sizeof(it), hipMemcpyDeviceToHost));
     {   // accounting build: requested bytes per launch by category
         unsigned long long tsum = 0;
-        for (int k = 0; k < MCEIK_TRAFFIC_N; k++) tsum += it[5 + k];
+        for (int k = 0; k < MCEIK_TRAFFIC_N; k++) tsum += it[6 + k];
         if (tsum && s->nlaunch) {
             static const char *nm[MCEIK_TRAFFIC_N] = {"own_load", "halo_load", "zup_load", "own_store",
                                                       "u0_store", "cell_load", "verify_load", "init_gather"};
             fprintf(stderr, "mceik traffic (requested bytes per FSM launch, %lld launches):", s->nlaunch);
-            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) fprintf(stderr, " %s=%.6e", nm[k], (double)it[5 + k] / s->nlaunch);
+            for (int k = 0; k < MCEIK_TRAFFIC_N; k++) fprintf(stderr, " %s=%.6e", nm[k], (double)it[6 + k] / s->nlaunch);
             fprintf(stderr, " total=%.6e\n", (double)tsum / s->nlaunch);
         }
     }
@@ -2290,6 +2353,15 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
         s->ev_folded = 0;
         HIPCHK(hipMemset(s->d_iters, 0, MCEIK_ITERS_N * sizeof(unsigned long long)));
     }
+    return 0;
+}
+
+extern "C" int mceik_mcmc_fsm_solves(mceik_mcmc *s, unsigned long long *solves)
+{
+    if (!s || !solves) return 1;
+    DeviceScope dg(s->device);
+    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipMemcpy(solves, s->d_iters + 5, sizeof(*solves), hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -1247,18 +1247,23 @@ __device__ __forceinline__ bool mc_next(const FsmLaunch &L, McQueue &q, int &sol
                 k = (int)(t / gs);
                 solve = clo * L.nstat + (int)(t - (unsigned)k * gs);
                 const int c = solve / L.nstat;
+                unsigned broken = 0;
                 if (lane == 0) {
                     // (a safety net, never expected: after ~30 s the wave stops
-                    // waiting, so a broken queue ends the launch instead of
-                    // hanging the GPU; the sync buffer's last word says so)
+                    // waiting, raises the sync buffer's broken-queue flag, which
+                    // the host reports as a failed run, and leaves the launch
+                    // without solving from a state that is not ready)
                     for (unsigned it = 0; atomicAdd(ready + c, 0) < k; it++) {
-                        if (it == (1u << 24)) {
+                        if (it >= L.mc_spin_limit) {
                             atomicExch(L.mc_sync + MC_SYNC_WORDS(L.nsolve / L.nstat) - 1, 1u);
+                            broken = 1;
                             break;
                         }
                         __builtin_amdgcn_s_sleep(32);
                     }
                 }
+                broken = __builtin_amdgcn_readfirstlane(__shfl(broken, 0, 64));
+                if (broken) return false;
                 __builtin_amdgcn_wave_barrier();
                 mc_l1_invalidate();
                 return true;
@@ -1371,9 +1376,16 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         float *u0 = reinterpret_cast<float *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
         const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
         // (a multi-step launch's model phase changes between steps: vector load)
-        const size_t sentry = !L.model_phase ? (size_t)model
-                                             : (size_t)model * L.nphase +
-                                                   (MC ? mcmcd::ldv(L.model_phase + model) : L.model_phase[model]);
+        const int phase = L.model_phase ? (MC ? mcmcd::ldv(L.model_phase + model) : L.model_phase[model])
+                                        : fsm_plain_phase(L, model);
+        if (L.skip && L.skip[phase * L.nstat + station]) {      // no picks of this phase at this station
+            skip_solve<float>(L, solve);
+            if (MC) mc_finish(L, (int)solve, mk);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            continue;
+        }
+        const size_t sentry = !L.model_phase ? (size_t)model : (size_t)model * L.nphase + phase;
         const void *slow_model = reinterpret_cast<const float *>(L.slow) + sentry * ncell;
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
                    sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
@@ -1448,6 +1460,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         if (lane == 0) {
             if (L.solve_clock) L.solve_clock[2 * (size_t)solve + 1] = __builtin_amdgcn_s_memrealtime();
             if (L.iter_total) atomicAdd(L.iter_total, (unsigned long long)iters);
+            if (L.solve_count) atomicAdd(L.solve_count, 1ull);
             if (L.niter) L.niter[solve] = iters;
             if (L.ierr) L.ierr[solve] = ierr;
         }

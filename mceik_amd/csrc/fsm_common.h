@@ -57,18 +57,29 @@ struct FsmLaunch {
     const float *ev_frac;        // [nev][3] trilinear fractions (ev_node = lowest corner), or null = node value
     const int *model_phase;      // slow_mode 1: model m uses slow entry m * nphase + model_phase[m], or null
     int nphase;
+    const unsigned char *skip;   // [nphase][nstat]: solve of (phase, station) skipped when set, or null
+    unsigned long long *solve_count;  // += solves executed, or null
     // Multi-step sampler launch (fsm16 kernel only; null mc_dev: a plain
     // batch).  Solves of steps mc_step0 .. mc_step0 + mc_nsteps - 1; the wave
     // that completes a chain's solves of a step runs the chain's accept, kept
     // state and next proposal (mcmc_device.h).  mc_sync: [8] group owner (XCD
     // id + 1) | [8][32] group tickets | [nchains] steps ready | [nchains]
-    // solves done | [1] broken-queue flag, zeroed before the launch.
+    // solves done (zeroed before every launch) | [1] broken-queue flag (zeroed
+    // once at init; the sampler checks it at every synchronisation).
     const void *mc_dev;          // the sampler's McmcDev (device copy)
     unsigned *mc_sync;
+    unsigned mc_spin_limit;      // polls of a step-ready wait before the queue counts as broken
     int mc_step0, mc_nsteps;
     int mc_nburn, mc_keepk, mc_maxs, mc_nkept0;   // kept-state slots (mceik_mcmc_run's bookkeeping)
 };
 #define MC_SYNC_WORDS(nchains) (8 + 8 * 32 + 2 * (nchains) + 1)
+
+// Phase of model m of a batch without a phase map: models [chain][phase]
+// when nphase > 1 (the sampler's full forward), else 0.
+static inline __host__ __device__ int fsm_plain_phase(const FsmLaunch &L, int m)
+{
+    return L.nphase > 1 ? m % L.nphase : 0;
+}
 
 // Inversion-grid slowness entry of model m (slow_mode 1).
 static inline __host__ __device__ size_t fsm_slow_entry(const FsmLaunch &L, int m)

@@ -156,6 +156,25 @@ __device__ __forceinline__ float event_time(const FsmLaunch &L, const R *u, int 
     return __fadd_rn(b0, __fmul_rn(wz, __fsub_rn(b1, b0)));
 }
 
+// A skipped solve (mceik_fsm_batch.skip: the station has no picks of the
+// solve's phase): no sweep; iterations 0, ierr 0, its table row FLT_MAX.
+template <typename R>
+__device__ __forceinline__ void skip_solve(const FsmLaunch &L, unsigned solve)
+{
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+        if (L.solve_clock) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            L.solve_clock[2 * (size_t)solve] = t;
+            L.solve_clock[2 * (size_t)solve + 1] = t;
+        }
+        if (L.niter) L.niter[solve] = 0;
+        if (L.ierr) L.ierr[solve] = 0;
+    }
+    if (L.ttab)
+        for (int e = lane; e < L.nev; e += 64) L.ttab[(size_t)solve * L.nev + e] = FLT_MAX;
+}
+
 // Per-solve boundary-condition boxes (EIKONAL3D_SETBCS nodes, lupd = .FALSE.).
 // Wave-uniform, kept in LDS: box k = {xlo, xhi, ylo, yhi, zlo, zhi} (0-based, inclusive).
 struct BcBoxes {

@@ -934,6 +934,13 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         const unsigned solve = (unsigned)snext;
         if (L.solve_clock && lane == 0) L.solve_clock[2 * (size_t)solve] = __builtin_amdgcn_s_memrealtime();
         const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
+        if (L.skip && L.skip[(L.model_phase && SLOWMODE != 0 ? L.model_phase[model] : fsm_plain_phase(L, model)) *
+                                 L.nstat + station]) {
+            skip_solve<R>(L, solve);                    // no picks of this phase at this station
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            continue;
+        }
         const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
         R *u = reinterpret_cast<R *>(L.u) + slot * L.field_elems;
         R *u0 = reinterpret_cast<R *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
@@ -1044,6 +1051,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         if (lane == 0) {
             if (L.solve_clock) L.solve_clock[2 * (size_t)solve + 1] = __builtin_amdgcn_s_memrealtime();
             if (L.iter_total) atomicAdd(L.iter_total, (unsigned long long)iters);
+            if (L.solve_count) atomicAdd(L.solve_count, 1ull);
             if (L.niter) L.niter[solve] = iters;
             if (L.ierr) L.ierr[solve] = ierr;
         }

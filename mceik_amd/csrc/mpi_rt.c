@@ -14,7 +14,9 @@
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <stddef.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #define MCEIK_HIDDEN __attribute__((visibility("hidden")))
 
@@ -72,6 +74,22 @@ static int load(void)
         rt.waitall = (waitall_fn)sym(h, "MPI_Waitall");
         rt.ok = rt.initialized && rt.finalized && rt.rank && rt.size && rt.bcast && rt.allreduce && rt.allgather &&
                 rt.isend && rt.irecv && rt.waitall;
+        // The handles passed below (MPI_INT, MPI_DOUBLE, MPI_IN_PLACE,
+        // MPI_Comm_f2c) are MPICH-ABI compile-time constants: an MPI of
+        // another ABI (Open MPI, e.g. through mpi4py or torch) would take them
+        // as pointers.  Only an MPICH-ABI library is used; any other counts
+        // as no MPI, said once.
+        typedef int (*libver_fn)(char *, int *);
+        libver_fn ver = (libver_fn)sym(h, "MPI_Get_library_version");
+        if (rt.ok) {
+            static char v[MPI_MAX_LIBRARY_VERSION_STRING];
+            int len = 0;
+            rt.ok = ver && ver(v, &len) == MPI_SUCCESS &&
+                    (strstr(v, "MPICH") || strstr(v, "Intel(R) MPI") || strstr(v, "MVAPICH"));
+            if (!rt.ok)
+                fprintf(stderr, "libmceik_hip: the loaded MPI is not MPICH-ABI (%.60s); "
+                                "the MPI entry points run as a single process\n", ver ? v : "no MPI_Get_library_version");
+        }
     }
     if (!rt.ok) return 0;
     int a = 0, b = 0;

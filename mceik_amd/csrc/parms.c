@@ -56,6 +56,8 @@ static const struct key KEYS[] = {
     O("mcmc", "vmin", K_INT, vmin), O("mcmc", "vmax", K_INT, vmax), O("mcmc", "dvmax", K_INT, dvmax),
     O("mcmc", "seed", K_U32, seed), O("mcmc", "max_samples", K_INT, max_samples),
     O("mcmc", "device", K_INT, device),
+    O("mcmc", "nphase", K_INT, nphase), O("mcmc", "vsmin", K_INT, vsmin), O("mcmc", "vsmax", K_INT, vsmax),
+    O("mcmc", "mask_s", K_INT, mask_s),
 };
 #define NKEYS ((int)(sizeof(KEYS) / sizeof(KEYS[0])))
 

@@ -66,6 +66,9 @@ class Problem:
     tt_interp: int = 0              # 0: event times at the nearest node (reference); 1: trilinear in the cell
     v_true: np.ndarray = None       # [ncell] int, model used to make the picks
     vs_true: np.ndarray = None      # [ncell] int, S model of the picks (P/S problems)
+    has_p: np.ndarray = None        # [nstat] lhasP (mceik_struct.h:43-46); None: stations with used P picks
+    has_s: np.ndarray = None        # [nstat] lhasS; None: stations with used S picks
+    lcartesian: int = 1             # mceik_stations_struct.lcartesian (the sampler takes metres only)
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -159,6 +162,24 @@ class Problem:
         corr = np.where(self.obs_phase == 1, sc[self.obs_stat], self.pcorr[self.obs_stat])
         return np.where(self.obs_mask == 0, corr, 0.0)
 
+    def station_flags(self):
+        """(lhasP, lhasS) [nstat] int: the explicit has_p / has_s, else whether
+        the station has a used pick of the phase (homog.c:230-235 sets them per
+        station from its picks).  The sampler solves a station's P (S) table
+        only when its flag is set."""
+        def has(t):
+            sel = (self.luse != 0) & (self.pick_type == t)
+            return np.array([bool((sel & (self.obs_stat == k)).any()) for k in range(self.nstat)], np.int32)
+        hp = np.asarray(self.has_p, np.int32) if self.has_p is not None else has(P_PRIMARY_PICK)
+        hs = np.asarray(self.has_s, np.int32) if self.has_s is not None else has(S_PRIMARY_PICK)
+        return hp, hs
+
+    @property
+    def skip(self):
+        """[nphase][nstat] uint8: solves the sampler skips (no picks of that phase)."""
+        hp, hs = self.station_flags()
+        return np.stack([hp == 0, hs == 0][:max(1, self.nphase)]).astype(np.uint8)
+
     @property
     def n_s_picks(self):
         k = self.obs_stat
@@ -190,13 +211,13 @@ class Problem:
         parms.nrefx, parms.nrefy, parms.nrefz = (int(v) for v in self.nref)
         st = _lib.StationsStruct()
         st.nstat = self.nstat
-        st.lcartesian = 1
+        st.lcartesian = int(self.lcartesian)
         st.xrec, st.yrec, st.zrec = dp(self.sx), dp(self.sy), dp(self.sz)
         st.pcorr = dp(self.pcorr)
         st.scorr = dp(self.scorr if self.scorr is not None else np.zeros(self.nstat))
-        has = lambda t: np.array([((self.obs_stat == k) & (self.pick_type == t)).any() for k in range(self.nstat)])
-        st.lhasP = ip(has(P_PRIMARY_PICK))
-        st.lhasS = ip(has(S_PRIMARY_PICK))
+        hp, hs = self.station_flags()
+        st.lhasP = ip(hp)
+        st.lhasS = ip(hs)
         cat = _lib.CatalogStruct()
         cat.nevents = self.nevents
         cat.xsrc, cat.ysrc, cat.zsrc = dp(self.ex), dp(self.ey), dp(self.ez)
@@ -352,7 +373,9 @@ class Sampler:
             self._last_full = False
 
     def sync(self):
-        self._L.mceik_mcmc_sync(self._h)
+        rc = self._L.mceik_mcmc_sync(self._h)
+        if rc != 0:
+            raise RuntimeError(f"mceik_mcmc_sync failed ({rc})")
 
     def info(self):
         """mceik_mcmc_get_info as a dict (pipes, kernel instance, waves, workspaces)."""
@@ -444,6 +467,14 @@ class Sampler:
         if self._L.mceik_mcmc_fsm_stats(self._h, C.byref(ms), C.byref(nl), C.byref(it), tv, int(reset)) != 0:
             raise RuntimeError("mceik_mcmc_fsm_stats failed")
         return ms.value, nl.value, it.value, tuple(tv)
+
+    def fsm_solves(self):
+        """Solves executed since init or the last fsm_stats(reset=True) (mceik_mcmc_fsm_solves;
+        solves of stations without picks of the phase are skipped, not counted)."""
+        n = C.c_ulonglong(0)
+        if self._L.mceik_mcmc_fsm_solves(self._h, C.byref(n)) != 0:
+            raise RuntimeError("mceik_mcmc_fsm_solves failed")
+        return n.value
 
     def samples(self, max_states=None, device_ptr=None):
         """Kept states [k, *model_shape] (host numpy, or copied into device_ptr)."""

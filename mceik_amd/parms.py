@@ -79,5 +79,10 @@ def apply_to_problem(p, parms, opts):
     p.nburn, p.keepk, p.niter = parms.mcparms.nburnIn, parms.mcparms.keepK, parms.mcparms.niter
     p.vmin, p.vmax, p.dvmax, p.seed = opts.vmin, opts.vmax, opts.dvmax, opts.seed
     p.tt_interp = opts.tt_interp
+    if opts.nphase > 1 and p.nphase != opts.nphase:
+        raise ValueError(f"configured nphase {opts.nphase} but the problem holds {p.nphase} model(s) per chain")
+    if opts.nphase > 1 or p.nphase > 1:
+        p.vsmin, p.vsmax = opts.vsmin or p.vsmin, opts.vsmax or p.vsmax
+    p.mask_s = opts.mask_s
     return dict(nchains=opts.nchains, chain_offset=opts.chain_offset, max_samples=opts.max_samples,
                 device=opts.device, precision=opts.precision or 32, max_waves=opts.max_waves)

@@ -296,6 +296,9 @@ typedef struct {
     int nphase;                   /* velocity models per chain: 1 = P, 2 = P and S (homog.c:208-258) */
     int vsmin, vsmax;             /* S prior (nphase 2) */
     const int *obs_phase;         /* NULL (all P) or [nobs] 0 = P, 1 = S: the model an observation fits */
+    const unsigned char *skip;    /* NULL or [nphase][nstat]: no table for (phase, station) -- the station
+                                     has no picks of that phase (lhasP / lhasS, homog.c:313-335); its
+                                     table row is FLT_MAX (the sampler's rule, mceik_fsm_batch.skip) */
 } oracle_mcmc_problem;
 
 /* Travel time of an event from a solved fp32 field u (x fastest).  w == NULL:
@@ -333,8 +336,20 @@ void oracle_expand_slowness(const oracle_mcmc_problem *p, const int *v, float *s
             }
 }
 
-/* travel-time table [station][event] (fp32) for one velocity model */
+/* travel-time table [station][event] (fp32) of phase ph's velocity model */
+static int oracle_forward_phase_f32(const oracle_mcmc_problem *p, int ph, const int *v, float *ttab, int *niter);
+
 int oracle_forward_f32(const oracle_mcmc_problem *p, const int *v, float *ttab, int *niter)
+{
+    return oracle_forward_phase_f32(p, 0, v, ttab, niter);
+}
+
+int oracle_forward_s_f32(const oracle_mcmc_problem *p, const int *v, float *ttab, int *niter)
+{
+    return oracle_forward_phase_f32(p, 1, v, ttab, niter);
+}
+
+static int oracle_forward_phase_f32(const oracle_mcmc_problem *p, int ph, const int *v, float *ttab, int *niter)
 {
     size_t n = (size_t)p->nx * p->ny * p->nz;
     float *slow = (float *)malloc(n * sizeof(float));
@@ -344,6 +359,11 @@ int oracle_forward_f32(const oracle_mcmc_problem *p, const int *v, float *ttab, 
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : nerr)
 #endif
     for (int s = 0; s < p->nstat; s++) {
+        if (p->skip && p->skip[(size_t)ph * p->nstat + s]) {
+            if (niter) niter[s] = 0;
+            for (int e = 0; e < p->nevents; e++) ttab[(size_t)s * p->nevents + e] = FLT_MAX;
+            continue;
+        }
         float *u = (float *)malloc(n * sizeof(float));
         double ts = 0.0;
         int it = 0;
@@ -420,7 +440,7 @@ int oracle_forward_all_f32(const oracle_mcmc_problem *p, const int *v, float *tt
 {
     const size_t ncell = (size_t)p->ncx * p->ncy * p->ncz, per = (size_t)p->nstat * p->nevents;
     int nerr = 0;
-    for (int ph = 0; ph < oracle_nphase(p); ph++) nerr += oracle_forward_f32(p, v + ph * ncell, ttab + ph * per, NULL);
+    for (int ph = 0; ph < oracle_nphase(p); ph++) nerr += oracle_forward_phase_f32(p, ph, v + ph * ncell, ttab + ph * per, NULL);
     return nerr;
 }
 

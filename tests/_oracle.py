@@ -129,7 +129,7 @@ class McmcProblem(C.Structure):
                                           "tobs", "tcorr", "var")] + \
                [("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int), ("seed", C.c_uint32),
                 ("ev_frac", C.c_void_p), ("nphase", C.c_int), ("vsmin", C.c_int), ("vsmax", C.c_int),
-                ("obs_phase", C.c_void_p)]
+                ("obs_phase", C.c_void_p), ("skip", C.c_void_p)]
 
 
 def make_problem(pb):
@@ -161,15 +161,25 @@ def make_problem(pb):
         a = np.ascontiguousarray(pb.obs_phase, dtype=np.int32)
         keep.append(a)
         P.obs_phase = a.ctypes.data
+    sk = getattr(pb, "skip", None)
+    if sk is not None and np.asarray(sk).any():
+        a = np.ascontiguousarray(sk, dtype=np.uint8)
+        keep.append(a)
+        P.skip = a.ctypes.data
     P._keep = keep
     return P
 
 
-def forward_f32(P, v):
+def forward_f32(P, v, phase=0):
+    """Tables [nstat][nev] and iterations of one model of phase `phase` (the
+    phase selects the skip row: stations without picks of it get FLT_MAX)."""
     tt = np.zeros(P.nstat * P.nevents, dtype=np.float32)
     it = np.zeros(P.nstat, dtype=np.int32)
     v = np.ascontiguousarray(v, dtype=np.int32)
-    lib().oracle_forward_f32(C.byref(P), _p(v), _p(tt), _p(it))
+    f = lib().oracle_forward_s_f32 if phase else lib().oracle_forward_f32
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p] * 4
+    f(C.byref(P), _p(v), _p(tt), _p(it))
     return tt.reshape(P.nstat, P.nevents), it
 
 

@@ -63,42 +63,45 @@ def test_c3_sampler_forward_bitwise_reused_scratch():
         assert logl0[c] == O.loglik(P, tt)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_c3_bench_production_launch_bitwise():
     """The bench's exact C3 launch: Sampler(C3) with 1024 chains and the
     library defaults (two pipes, occupancy-many waves, two workspaces).
     Chains {0, 1, 511, 512, 1022, 1023} straddle the pipe split: their init
-    tables, iteration counts and logL == the fp32 twin, and their models and
-    logL after one step == oracle_mcmc_run."""
+    tables, iteration counts and logL == the fp32 twin, and their models,
+    logL and accept counts after three steps == oracle_mcmc_run."""
     _dev()
     from mceik_amd import mcmc
     p = _problem("C3")
     p.dvmax = 400
     p.var[:] = 1e-6
+    nsteps = 3
     s = mcmc.Sampler(p, nchains=1024)
     info = s.info()
     assert info["npipe"] == 2 and info["chains"] == [512, 512]
-    assert info["step_z"] == 16 and info["fixed_layout"]
+    assert info["step_z"] == 16 and info["fixed_layout"] and not info["multi_step"]
     assert info["kernel"] == "fsm16_solve_kernel<2, 1>"
     assert min(info["waves"]) >= 1024, info           # the full-occupancy launch (2048 on a 256-CU MI355X)
     v0, logl0, _, _ = s.state()
     ttab, niter, _, ierr = s.last(with_ierr=True)
     assert not ierr.any()
-    s.run(1)
-    v1, logl1, _, step = s.state()
+    s.run(nsteps)
+    v1, logl1, nacc1, step = s.state()
     _, nl, _, _ = s.fsm_stats()
     s.close()
-    assert step == 1 and nl == 2                      # one timed half launch per pipe
+    assert step == nsteps and nl == 2 * nsteps        # one timed half launch per pipe and step
     P = O.make_problem(p)
-    chains = (0, 1, 511, 512, 1022, 1023)
-    for c in chains:
+    for c in (0, 1, 511, 512, 1022, 1023):
         tt, it = O.forward_f32(P, v0[c])
         assert np.array_equal(ttab[c].view(np.uint32), tt.view(np.uint32)), c
         assert np.array_equal(niter[c], it), c
         assert logl0[c] == O.loglik(P, tt), c
-        vo, lo, _, _ = O.mcmc_run(P, v0[c:c + 1], logl0[c:c + 1], c, 0, 1)
-        assert np.array_equal(v1[c], vo[0]), c
-        assert logl1[c].view(np.uint64) == lo[0].view(np.uint64), c
+    for c in (0, 511, 1022):                          # pairs of consecutive global ids
+        sl = slice(c, c + 2)
+        vo, lo, acc, _ = O.mcmc_run(P, v0[sl], logl0[sl], c, 0, nsteps)
+        assert np.array_equal(v1[sl], vo), c
+        assert np.array_equal(logl1[sl].view(np.uint64), lo.view(np.uint64)), c
+        assert np.array_equal(nacc1[sl], acc.sum(0)), c
 
 
 @pytest.mark.timeout(600)
@@ -126,6 +129,41 @@ def test_c5_sampler_launch_bitwise():
     tt, it = O.forward_f32(P, v0[0])
     assert np.array_equal(ttab[0, :8].view(np.uint32), tt.view(np.uint32))
     assert np.array_equal(niter[0, :8], it)
+
+
+@pytest.mark.timeout(900)
+def test_c5_bench_load_launch_bitwise():
+    """C5 at the bench's per-GPU load: 256 chains x 64 stations at 256^3 =
+    16384 solves per step on scratch-budget-capped waves in ONE pipe (the
+    library refuses to split capped waves), several solves per wave.  Chains 0
+    and 255, 8 stations each: the init tables and the first step's tables of
+    the proposed models == the fp32 twin."""
+    _dev()
+    torch.cuda.empty_cache()
+    from mceik_amd import mcmc
+    p = mcmc.make_problem("C5", picks="analytic")
+    s = mcmc.Sampler(p, nchains=256)
+    info = s.info()
+    assert info["npipe"] == 1 and info["kernel"] == "fsm16_solve_kernel<0, 4>", info
+    assert sum(info["waves"]) < 256 * 64 / 4, info   # budget-capped: several solves per wave
+    v0, _, _, _ = s.state()
+    ttab0, niter0, _, ierr = s.last(with_ierr=True)
+    assert not ierr.any()
+    s.run(1)
+    ttab1, niter1, _ = s.last()
+    s.close()
+    P = O.make_problem(p)
+    P.nstat = 8                                       # the first 8 stations (same arrays)
+    for c in (0, 255):
+        tt, it = O.forward_f32(P, v0[c])
+        assert np.array_equal(ttab0[c, :8].view(np.uint32), tt.view(np.uint32)), c
+        assert np.array_equal(niter0[c, :8], it), c
+        cell, vn, inp, _ = O.propose(P, c, 0, v0[c])
+        vp = v0[c].copy()
+        vp[cell] = vn                                 # the step forwards the proposed model
+        tt, it = O.forward_f32(P, vp)
+        assert np.array_equal(ttab1[c, :8].view(np.uint32), tt.view(np.uint32)), c
+        assert np.array_equal(niter1[c, :8], it), c
 
 
 def test_c3_mcmc_two_steps_bitwise():

@@ -84,3 +84,25 @@ def test_multi_step_few_chains_vs_oracle(monkeypatch):
     assert np.array_equal(v, vo)
     assert np.array_equal(logl.view(np.uint64), lo.view(np.uint64))
     assert 0 < acco.sum()
+
+
+def test_multi_step_broken_queue_is_reported(monkeypatch):
+    """A multi-step wave that gives up waiting for a chain's previous step
+    (the ~30-s safety net; MCEIK_MC_SPIN_LIMIT=0 makes every wait give up at
+    once) leaves the launch without solving from unready state, and the
+    sampler reports the failure at the next synchronisation instead of
+    returning corrupt chains."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("P")
+    monkeypatch.setenv("MCEIK_PERSIST", "1")
+    monkeypatch.setenv("MCEIK_PIPES", "1")
+    monkeypatch.setenv("MCEIK_MC_SPIN_LIMIT", "0")
+    s = mcmc.Sampler(p, nchains=64, max_samples=8)
+    assert s.info()["multi_step"]
+    s.run(8)
+    with pytest.raises(RuntimeError):
+        s.sync()
+    with pytest.raises(RuntimeError):
+        s.state()
+    s.close()

@@ -206,3 +206,56 @@ def test_ps_posterior_writes_s_tables(tmp_path):
                                                 np.array([[0.0, p.sx[st], p.sy[st], p.sz[st]]]), maxit=p.maxit,
                                                 tol=p.tol, dtype=np.float32)
                     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (m, ph, st)
+
+
+@pytest.mark.parametrize("mode", ["pipes2", "multi"])
+def test_station_flags_skip_solves_bitwise(mode, monkeypatch):
+    """Half the stations have no S picks (lhasS = 0, homog.c:313-335 makes no
+    table for them): their S solves are skipped (table FLT_MAX, niter 0), the
+    P tables of every station and the S tables of the others are the twin's,
+    logL, accept sequence and both models after 6 steps == oracle_mcmc_run
+    (with the same skip rule), and mceik_mcmc_fsm_solves counts only the
+    solves that ran."""
+    _dev()
+    monkeypatch.setenv("MCEIK_PERSIST", "1" if mode == "multi" else "0")
+    monkeypatch.setenv("MCEIK_PIPES", "2" if mode == "pipes2" else "1")
+    from mceik_amd import mcmc
+    p = _ps_problem(nstat=6)
+    nos = np.arange(p.nstat) % 2 == 1                     # stations 1, 3, 5: no S picks
+    p.luse[(p.pick_type == mcmc.S_PRIMARY_PICK) & nos[p.obs_stat]] = 0
+    hp, hs = p.station_flags()
+    assert hp.all() and np.array_equal(hs, (~nos).astype(np.int32))
+    nch, off, nsteps = 4, 3, 6
+    s = mcmc.Sampler(p, nchains=nch, chain_offset=off)
+    assert s.info()["multi_step"] == (mode == "multi")
+    v0, logl0, _, _ = s.state()
+    tt, niter, _, ierr = s.last(with_ierr=True)
+    assert not ierr.any()
+    assert (tt[:, 1, nos] == np.float32(np.finfo(np.float32).max)).all() and (niter[:, 1, nos] == 0).all()
+    P = O.make_problem(p)
+    for c in range(nch):
+        to = O.forward_all_f32(P, v0[c])
+        assert np.array_equal(tt[c].view(np.uint32), to.view(np.uint32)), c
+        for ph in range(2):
+            _, it = O.forward_f32(P, v0[c, ph], phase=ph)
+            assert np.array_equal(niter[c, ph], it), (c, ph)
+        assert logl0[c] == O.loglik(P, to)
+    assert s.fsm_solves() == 0                            # init's forward is not counted
+    acc, trace, phases = [], [], []
+    for _ in range(nsteps):
+        s.run(1)
+        _, _, a = s.last()
+        _, lg, _, _ = s.state()
+        acc.append(a.copy())
+        trace.append(lg.copy())
+        phases.append(s.last_phase())
+    v, logl, _, _ = s.state()
+    solves = s.fsm_solves()
+    s.close()
+    ph = np.array(phases)
+    assert (ph == 1).any()
+    assert solves == int((ph == 0).sum()) * p.nstat + int((ph == 1).sum()) * int((~nos).sum())
+    vo, lo, acco, traceo = O.mcmc_run(P, v0, logl0, off, 0, nsteps)
+    assert np.array_equal(np.array(acc), acco)
+    assert np.array_equal(np.array(trace).view(np.uint64), traceo.view(np.uint64))
+    assert np.array_equal(v, vo) and np.array_equal(logl.view(np.uint64), lo.view(np.uint64))

@@ -37,6 +37,10 @@ nchains = 256
 seed = 0xfffffff0
 vmin = 2000
 vmax = 8000
+nphase = 2
+vsmin = 900
+vsmax = 5000
+mask_s = 1
 """
 
 
@@ -59,6 +63,7 @@ def test_read_file_and_overrides(tmp_path):
     assert (parms.mcparms.nburnIn, parms.mcparms.niter, parms.mcparms.keepK) == (10, 500, 5)
     assert opts.nchains == 64 and opts.seed == 0xfffffff0 and (opts.vmin, opts.vmax) == (2000, 8000)
     assert opts.dvmax == 50                                        # untouched default
+    assert (opts.nphase, opts.vsmin, opts.vsmax, opts.mask_s) == (2, 900, 5000, 1)
 
 
 def test_write_read_roundtrip(tmp_path):
@@ -69,6 +74,7 @@ def test_write_read_roundtrip(tmp_path):
     PM.write(g, parms, opts)
     p2, o2 = PM.load(g, base=(_lib.MceikParms(), _lib.McmcOpts()))
     assert bytes(p2) == bytes(parms) and bytes(o2) == bytes(opts)
+    assert (o2.nphase, o2.vsmin, o2.vsmax, o2.mask_s) == (2, 900, 5000, 1)    # a joint P/S run stays joint
 
 
 @pytest.mark.parametrize("text, line", [("[grid]\nnx = 4x\n", 2), ("[grid]\nbogus = 1\n", 2),
@@ -107,10 +113,13 @@ def test_apply_to_problem(tmp_path):
     f = tmp_path / "run.ini"
     f.write_text(INI.replace("ny = 36", "ny = 40").replace("nz = 30", "nz = 40").replace("nrefz = 2", "nrefz = 4"))
     parms, opts = PM.load(f)
-    p = mcmc.make_problem("C2", n=40, nstat=3, nev=2)
+    p = mcmc.make_problem("C2", n=40, nstat=3, nev=2, phases="PS")
     kw = PM.apply_to_problem(p, parms, opts)
+    assert (p.vsmin, p.vsmax, p.mask_s) == (900, 5000, 1)
     assert kw["nchains"] == 256 and kw["precision"] == 32
     assert p.h == 250.0 and p.x0 == 100.5 and p.nref == (4, 4, 4) and p.tt_interp == 1
     assert p.niter == 500 and p.maxit == 12 and np.isclose(p.tol, 1e-7)
     with pytest.raises(ValueError):
         PM.apply_to_problem(mcmc.make_problem("C2", n=24, nstat=3, nev=2), parms, opts)
+    with pytest.raises(ValueError):                                # nphase 2 configured, a P-only problem
+        PM.apply_to_problem(mcmc.make_problem("C2", n=40, nstat=3, nev=2), parms, opts)
