@@ -12,6 +12,7 @@
 #ifndef MCEIK_H5IO_H_AMD
 #define MCEIK_H5IO_H_AMD 1
 #include <limits.h>
+#include <stdbool.h>
 #include <stdint.h>
 #ifndef PATH_MAX
 #define PATH_MAX 4096
@@ -26,7 +27,7 @@ enum { MCEIK_H5_TRAVELTIME_FILE = 1, MCEIK_H5_LOCATION_FILE = 2 };   /* h5io.h:1
 /* h5io.c:9-58: "<dir>/<proj>_ttimes.h5" (job 1) or "_locations.h5" (job 2). */
 int eikonal_h5io_setFileName(int job, const char *dirnm, const char *projnm, char fileName[PATH_MAX]);
 /* h5io.c:164-181 / 183-190 */
-void eikonal_h5io_setTravelTimeName(int model, int station, int isP, char dataSetName[512]);
+void eikonal_h5io_setTravelTimeName(int model, int station, bool isP, char dataSetName[512]);
 void eikonal_h5io_setLocationName(int model, int event, char dataSetName[512]);
 
 /* Replaces eikonal_h5io_initTTables (h5io.c:559-712): /Model/{x,y,z}locs and

@@ -16,6 +16,7 @@
  * writes whole grids (ix0 = iy0 = iz0 = 0, nxLoc = nx ...).
  */
 #include <limits.h>
+#include <stdbool.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -52,7 +53,7 @@ int eikonal_h5io_setFileName(int job, const char *dirnm, const char *projnm, cha
     return 0;
 }
 
-void eikonal_h5io_setTravelTimeName(int model, int station, int isP, char dataSetName[512])
+void eikonal_h5io_setTravelTimeName(int model, int station, bool isP, char dataSetName[512])
 {
     memset(dataSetName, 0, 512);
     snprintf(dataSetName, 512, "/TravelTimeTables/Model_%d/Station_%d/%sTravelTimes", model, station,

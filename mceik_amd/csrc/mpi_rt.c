@@ -18,7 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define MCEIK_HIDDEN __attribute__((visibility("hidden")))
+#include "mpi_rt.h"
 
 #if defined(__has_include)
 #if __has_include(<mpi.h>)
@@ -37,6 +37,9 @@ typedef int (*allgather_fn)(const void *, int, MPI_Datatype, void *, int, MPI_Da
 typedef int (*isend_fn)(const void *, int, MPI_Datatype, int, int, MPI_Comm, MPI_Request *);
 typedef int (*irecv_fn)(void *, int, MPI_Datatype, int, int, MPI_Comm, MPI_Request *);
 typedef int (*waitall_fn)(int, MPI_Request *, MPI_Status *);
+typedef int (*gather_fn)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, int, MPI_Comm);
+typedef int (*scatter_fn)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, int, MPI_Comm);
+typedef int (*barrier_fn)(MPI_Comm);
 
 static struct {
     int tried, ok;
@@ -48,6 +51,9 @@ static struct {
     isend_fn isend;
     irecv_fn irecv;
     waitall_fn waitall;
+    gather_fn gather;
+    scatter_fn scatter;
+    barrier_fn barrier;
 } rt;
 
 static void *sym(void *h, const char *name)
@@ -72,8 +78,11 @@ static int load(void)
         rt.isend = (isend_fn)sym(h, "MPI_Isend");
         rt.irecv = (irecv_fn)sym(h, "MPI_Irecv");
         rt.waitall = (waitall_fn)sym(h, "MPI_Waitall");
+        rt.gather = (gather_fn)sym(h, "MPI_Gather");
+        rt.scatter = (scatter_fn)sym(h, "MPI_Scatter");
+        rt.barrier = (barrier_fn)sym(h, "MPI_Barrier");
         rt.ok = rt.initialized && rt.finalized && rt.rank && rt.size && rt.bcast && rt.allreduce && rt.allgather &&
-                rt.isend && rt.irecv && rt.waitall;
+                rt.isend && rt.irecv && rt.waitall && rt.gather && rt.scatter && rt.barrier;
         // The handles passed below (MPI_INT, MPI_DOUBLE, MPI_IN_PLACE,
         // MPI_Comm_f2c) are MPICH-ABI compile-time constants: an MPI of
         // another ABI (Open MPI, e.g. through mpi4py or torch) would take them
@@ -144,6 +153,35 @@ MCEIK_HIDDEN int mceik_mpi_allgather_bytes(int fcomm, const void *mine, void *al
                    MPI_SUCCESS ? 0 : -1;
 }
 
+/* Fixed-size byte records: root receives every rank's `mine` into `all`
+ * (rank order) / sends record r of `all` to rank r; a byte broadcast; a
+ * barrier (the h5io and broadcast entry points, csrc/h5io_mpi.c, broadcast.c). */
+MCEIK_HIDDEN int mceik_mpi_gather_bytes(int fcomm, const void *mine, void *all, long long nbytes, int root)
+{
+    if (!load() || nbytes < 0 || nbytes > 0x7fffffffLL) return -1;
+    return rt.gather(mine, (int)nbytes, MPI_BYTE, all, (int)nbytes, MPI_BYTE, root, MPI_Comm_f2c((MPI_Fint)fcomm)) ==
+                   MPI_SUCCESS ? 0 : -1;
+}
+
+MCEIK_HIDDEN int mceik_mpi_scatter_bytes(int fcomm, const void *all, void *mine, long long nbytes, int root)
+{
+    if (!load() || nbytes < 0 || nbytes > 0x7fffffffLL) return -1;
+    return rt.scatter(all, (int)nbytes, MPI_BYTE, mine, (int)nbytes, MPI_BYTE, root, MPI_Comm_f2c((MPI_Fint)fcomm)) ==
+                   MPI_SUCCESS ? 0 : -1;
+}
+
+MCEIK_HIDDEN int mceik_mpi_bcast_bytes(int fcomm, void *v, long long nbytes, int root)
+{
+    if (!load() || nbytes < 0 || nbytes > 0x7fffffffLL) return -1;
+    return rt.bcast(v, (int)nbytes, MPI_BYTE, root, MPI_Comm_f2c((MPI_Fint)fcomm)) == MPI_SUCCESS ? 0 : -1;
+}
+
+MCEIK_HIDDEN int mceik_mpi_barrier(int fcomm)
+{
+    if (!load()) return -1;
+    return rt.barrier(MPI_Comm_f2c((MPI_Fint)fcomm)) == MPI_SUCCESS ? 0 : -1;
+}
+
 /* nmsg messages: send[k] (count[k] doubles to peer[k], tag tag[k]) when
  * dir[k] = 0, receive (from peer[k]) when dir[k] = 1; all complete on return. */
 MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, const int *peer, const int *tag,
@@ -193,4 +231,20 @@ MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, 
     (void)fcomm; (void)nmsg; (void)dir; (void)peer; (void)tag; (void)buf; (void)count;
     return -1;
 }
+MCEIK_HIDDEN int mceik_mpi_gather_bytes(int fcomm, const void *mine, void *all, long long nbytes, int root)
+{
+    (void)fcomm; (void)mine; (void)all; (void)nbytes; (void)root;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_scatter_bytes(int fcomm, const void *all, void *mine, long long nbytes, int root)
+{
+    (void)fcomm; (void)all; (void)mine; (void)nbytes; (void)root;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_bcast_bytes(int fcomm, void *v, long long nbytes, int root)
+{
+    (void)fcomm; (void)v; (void)nbytes; (void)root;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_barrier(int fcomm) { (void)fcomm; return -1; }
 #endif
