@@ -1982,7 +1982,7 @@ extern "C" int mceik_mcmc_init(const struct mceik_parms_struct *parms, const str
     b.max_waves = o->max_waves > 0 ? o->max_waves : 0;
     // f = h/v stays a normal float: the short correctly rounded sqrt (fp32 only)
     const int vhi = nphase == 2 ? std::max(o->vmax, o->vsmax) : o->vmax;
-    b.fast_sqrt = b.precision == 32 && parms->dx / (double)vhi >= 1e-12 ? 1 : 0;
+    b.fast_sqrt = parms->dx / (double)vhi >= 1e-12 ? 1 : 0;      // f = h*s >= 1e-12: the short sqrt (fp32, fp64)
     // the full batch (init, restore): every model of every chain, models
     // [chain][phase] in place of model_phase, tables into ttab_cur
     s->fb_all = b;

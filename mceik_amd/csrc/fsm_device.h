@@ -323,8 +323,7 @@ __device__ __forceinline__ float godunov_v(float a, float b, float c, float f, f
 template <bool FAST>
 __device__ __forceinline__ double godunov_v(double a, double b, double c, double f, double, double, double)
 {
-    int e;
-    return MCEIK_F64_SELECT ? godunov_sel(a, b, c, f, e) : godunov(a, b, c, f, e);
+    return godunov_fast64<FAST>(a, b, c, f);
 }
 
 // ---- per-solve setup: u = u_nan, then the source boxes (EIKONAL3D_SETBCS) ----

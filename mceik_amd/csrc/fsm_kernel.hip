@@ -1126,7 +1126,10 @@ static int occupancy_of(size_t lds)
 static int variant(const FsmLaunch &L, int is_double)
 {
     const int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
-    if (is_double) return 9 + mode * 2 + (mode == 2 && L.nrz == 4 && L.ccb <= 64 ? (L.kb == MCEIK_KB ? 2 : 1) : 0);
+    if (is_double) {
+        const int v = 9 + mode * 2 + (mode == 2 && L.nrz == 4 && L.ccb <= 64 ? (L.kb == MCEIK_KB ? 2 : 1) : 0);
+        return v == 15 && L.fast_sqrt ? 16 : v;      // the fp64 sampler instance with the short sqrt
+    }
     if (mode != 2) return mode * 2;
     return 4 + (L.fast_sqrt ? 1 : 0) + (L.nrz == 4 && L.fast_sqrt && L.ccb <= 64 ? (L.kb == MCEIK_KB ? 3 : 2) : 0);
 }
@@ -1142,7 +1145,8 @@ static int variant(const FsmLaunch &L, int is_double)
     X(11, double, 1, false, -1, 1, 0)           \
     X(13, double, 2, false, -1, 4, 0)           \
     X(14, double, 2, false, 2, 1, 0)            \
-    X(15, double, 2, false, 2, 1, MCEIK_KB)
+    X(15, double, 2, false, 2, 1, MCEIK_KB)     \
+    X(16, double, 2, true, 2, 1, MCEIK_KB)
 
 // the 16-z-step kernel (fsm16_kernel.hip) serves the fp32 cell-cache
 // instances (variants 7, 8) when fsm16_eligible(); MCEIK_FSM16=0 keeps the
@@ -1178,6 +1182,7 @@ const char *fsm_launch_name(const FsmLaunch &L, int is_double)
     case 13: return "fsm_solve_kernel<double, 2, false, -1, 4, 0>";
     case 14: return "fsm_solve_kernel<double, 2, false, 2, 1, 0>";
     case 15: return "fsm_solve_kernel<double, 2, false, 2, 1, 4>";
+    case 16: return "fsm_solve_kernel<double, 2, true, 2, 1, 4>";
     }
     return "?";
 }

@@ -143,10 +143,27 @@ __device__ __forceinline__ double godunov_sel(double a, double b, double c, doub
 // bits, +-0 and negatives do not).  Same values as the compare/select form
 // without its compare -> lane-mask -> select hazard wait states (gfx950 puts
 // two wait states between a VALU write of an SGPR mask and its use).
+#ifndef MCEIK_SQRT_ONESIDED
+#define MCEIK_SQRT_ONESIDED 0    // 1: only the upper test (v_sqrt_f32 never above the correctly rounded
+                                 // root), -1: only the lower test (never below); see tools/sqrt_dir_probe.hip
+#endif
 __device__ __forceinline__ float sqrt_normal(float x)
 {
     const float s = __builtin_amdgcn_sqrtf(x);
     const int sb = __builtin_bit_cast(int, s);
+#if MCEIK_SQRT_ONESIDED != 0
+    {
+        // The exhaustive probe (tools/sqrt_dir_probe.hip) shows the hardware
+        // root is off by at most one ulp and only on one side over the domain
+        // x >= 2^-104, so one Tuckerman test decides: +1 ulp when x > up*s
+        // (MCEIK_SQRT_ONESIDED 1), -1 ulp unless x > dn*s (-1).
+        const float t = __builtin_bit_cast(float, sb + MCEIK_SQRT_ONESIDED);
+        const int e = __builtin_bit_cast(int, __builtin_fmaf(-t, s, x));
+        int p;
+        asm("v_med3_i32 %0, %1, 0, 1" : "=v"(p) : "v"(e));
+        return __builtin_bit_cast(float, MCEIK_SQRT_ONESIDED > 0 ? sb + p : (sb - 1) + p);
+    }
+#endif
     const float dn = __builtin_bit_cast(float, sb - 1);
     const float up = __builtin_bit_cast(float, sb + 1);
     const int edn = __builtin_bit_cast(int, __builtin_fmaf(-dn, s, x));
@@ -174,6 +191,71 @@ __device__ __forceinline__ float sqrt_normal(float x)
     const float t = __builtin_bit_cast(float, edn) <= 0.0f ? dn : s;
     return __builtin_bit_cast(float, eup) > 0.0f ? up : t;
 #endif
+}
+
+// min / max of two doubles as single instructions.  In IEEE mode the
+// compiler quiets both operands of v_min_f64 / v_max_f64 first (a
+// canonicalising v_max_f64 x, x, x per operand not known to be the result of
+// arithmetic: every value loaded from LDS or HBM) in case one is a signalling
+// NaN; travel times, slownesses and their sums are never NaN, so the bare
+// instruction returns the same value.
+__device__ __forceinline__ double dmin_(double a, double b)
+{
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double dmax_(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// Correctly rounded fp64 sqrt for normal positive x below +inf: LLVM's
+// expansion of __builtin_sqrt (v_rsq_f64 and two Newton-Raphson / Goldschmidt
+// corrections, the same operations in the same order) without its input
+// scaling for x < 2^-767 and its +-0 / +inf fix-up, so the result is bitwise
+// __builtin_sqrt's for every such x.  Used only where the radicand finally
+// selected is provably normal: the 2D radicand 2f^2 - (a1 - a2)^2 > f^2 when
+// |a1 - a2| < f, the 3D one (4/9)(3f^2 - sum of the squared pairwise
+// differences) > (4/9) f^2 when the 3D case is taken, and the host validates
+// f = h * s >= 1e-12 (fp32's sqrt_normal, the same bound).  An unselected
+// radicand may be anything: a negative or zero one gives NaN, never selected.
+__device__ __forceinline__ double sqrt_normal_f64(double x)
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
+
+// The literal fp64 update for the fast path (no ierr): godunov_sel's values
+// with the sort and the minima as bare v_min_f64 / v_max_f64, the 2D root
+// computed unconditionally (no divergent branch), and (FAST) the short sqrt.
+// min(a1, a2) + f of the 2D fallback is x1 (a1 <= a2 by the sort).
+template <bool FAST>
+__device__ __forceinline__ double godunov_fast64(double a, double b, double c, double f)
+{
+    const double UN = DBL_MAX;
+    const double mn = dmin_(a, b), mx = dmax_(a, b);
+    const double a1 = dmin_(mn, c), a3 = dmax_(mx, c), a2 = dmax_(mn, dmin_(mx, c));
+    const double x1 = a1 + f;
+    const double amb = a1 - a2;
+    const double arg = (2.0 * f) * f - amb * amb;
+    const double s2 = FAST ? sqrt_normal_f64(arg) : __builtin_sqrt(arg);
+    const double x2 = __builtin_fabs(amb) < f ? 0.5 * ((a1 + a2) + s2) : x1;
+    const double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
+    const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
+    const double disc = qb * qb - 4.0 * qc;
+    const double x3 = 0.5 * (-qb + (FAST ? sqrt_normal_f64(disc) : __builtin_sqrt(disc)));
+    const bool r1 = !(x1 > a2), r2 = !(x2 > a3), nan_in = a1 == UN;
+    return nan_in ? UN : r1 ? x1 : r2 ? x2 : (x3 < UN ? x3 : UN);
 }
 
 // Branchless fp32 Godunov update, values and ierr identical to the twin
@@ -221,6 +303,6 @@ __device__ __forceinline__ float fmin_(float a, float b)
     const unsigned ia = __builtin_bit_cast(unsigned, a), ib = __builtin_bit_cast(unsigned, b);
     return __builtin_bit_cast(float, __builtin_elementwise_min(ia, ib));
 }
-__device__ __forceinline__ double fmin_(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double fmin_(double a, double b) { return dmin_(a, b); }
 
 }  // namespace

@@ -1,0 +1,36 @@
+#!/usr/bin/env bash
+# On the GPU box: the r04 evidence set for the current kernels.
+#  1 rocprofv3 kernel-trace stats of the default bench (fp32 two pipes + the fp64 record)
+#  2 fp32, one pipe, the timed launch: raw visit counters, PMC FETCH_SIZE; WRITE_SIZE; SQ
+#  3 fp64 (--precision 64), one pipe: the same
+#  4 the N = 2 flow rehearsed on one GPU (MCEIK_BENCH_REHEARSAL=1, gloo)
+# Outputs under gpurun_out/${M_OUT:-m04}/.  Every step under its own time limit.
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${M_OUT:-m04}
+mkdir -p "$O"
+( while sleep 45; do echo "[measure_r04] $(date +%T) running"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null || true' EXIT
+SQ="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES"
+echo "[measure_r04] trace"
+timeout -k 10 480 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --f64-steps 2 > "$O/bench_under_trace.log" 2>&1
+for prec in 32 64; do
+  if [ $prec = 32 ]; then K=fsm16_solve_kernel; else K="fsm_solve_kernel<double, 2, true"; fi
+  echo "[measure_r04] fp$prec raw"
+  timeout -k 10 300 python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --pipes 1 --raw-stats --precision $prec \
+      > "$O/bench_f${prec}_pipes1_raw.log" 2>&1
+  i=0
+  for P in FETCH_SIZE WRITE_SIZE "$SQ"; do
+    i=$((i+1))
+    echo "[measure_r04] fp$prec pmc$i"
+    timeout -k 10 400 rocprofv3 --pmc $P --kernel-include-regex "$K" -d "$O/f${prec}_pmc$i" -o pmc \
+        --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --pipes 1 --precision $prec \
+        > "$O/bench_f${prec}_pmc$i.log" 2>&1
+  done
+done
+echo "[measure_r04] rehearsal"
+MCEIK_BENCH_REHEARSAL=1 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 2 --warmup 1 > "$O/bench_rehearsal_n2.log" 2>&1
+echo done > "$O/DONE"
