@@ -40,6 +40,9 @@ typedef int (*waitall_fn)(int, MPI_Request *, MPI_Status *);
 typedef int (*gather_fn)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, int, MPI_Comm);
 typedef int (*scatter_fn)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, int, MPI_Comm);
 typedef int (*barrier_fn)(MPI_Comm);
+typedef int (*dup_fn)(MPI_Comm, MPI_Comm *);
+typedef int (*split_fn)(MPI_Comm, int, int, MPI_Comm *);
+typedef int (*free_fn)(MPI_Comm *);
 
 static struct {
     int tried, ok;
@@ -54,6 +57,9 @@ static struct {
     gather_fn gather;
     scatter_fn scatter;
     barrier_fn barrier;
+    dup_fn dup;
+    split_fn split;
+    free_fn cfree;
 } rt;
 
 static void *sym(void *h, const char *name)
@@ -81,8 +87,12 @@ static int load(void)
         rt.gather = (gather_fn)sym(h, "MPI_Gather");
         rt.scatter = (scatter_fn)sym(h, "MPI_Scatter");
         rt.barrier = (barrier_fn)sym(h, "MPI_Barrier");
+        rt.dup = (dup_fn)sym(h, "MPI_Comm_dup");
+        rt.split = (split_fn)sym(h, "MPI_Comm_split");
+        rt.cfree = (free_fn)sym(h, "MPI_Comm_free");
         rt.ok = rt.initialized && rt.finalized && rt.rank && rt.size && rt.bcast && rt.allreduce && rt.allgather &&
-                rt.isend && rt.irecv && rt.waitall && rt.gather && rt.scatter && rt.barrier;
+                rt.isend && rt.irecv && rt.waitall && rt.gather && rt.scatter && rt.barrier && rt.dup && rt.split &&
+                rt.cfree;
         // The handles passed below (MPI_INT, MPI_DOUBLE, MPI_IN_PLACE,
         // MPI_Comm_f2c) are MPICH-ABI compile-time constants: an MPI of
         // another ABI (Open MPI, e.g. through mpi4py or torch) would take them
@@ -182,6 +192,33 @@ MCEIK_HIDDEN int mceik_mpi_barrier(int fcomm)
     return rt.barrier(MPI_Comm_f2c((MPI_Fint)fcomm)) == MPI_SUCCESS ? 0 : -1;
 }
 
+/* Communicator construction for mpiutils.c (Fortran handles in and out):
+ * a duplicate, a split by colour (key = rank), and a free. */
+MCEIK_HIDDEN int mceik_mpi_comm_dup(int fcomm, int *fout)
+{
+    if (!load()) return -1;
+    MPI_Comm c;
+    if (rt.dup(MPI_Comm_f2c((MPI_Fint)fcomm), &c) != MPI_SUCCESS) return -1;
+    *fout = (int)MPI_Comm_c2f(c);
+    return 0;
+}
+
+MCEIK_HIDDEN int mceik_mpi_comm_split(int fcomm, int color, int key, int *fout)
+{
+    if (!load()) return -1;
+    MPI_Comm c;
+    if (rt.split(MPI_Comm_f2c((MPI_Fint)fcomm), color, key, &c) != MPI_SUCCESS) return -1;
+    *fout = (int)MPI_Comm_c2f(c);
+    return 0;
+}
+
+MCEIK_HIDDEN int mceik_mpi_comm_free(int fcomm)
+{
+    if (!load()) return -1;
+    MPI_Comm c = MPI_Comm_f2c((MPI_Fint)fcomm);
+    return rt.cfree(&c) == MPI_SUCCESS ? 0 : -1;
+}
+
 /* nmsg messages: send[k] (count[k] doubles to peer[k], tag tag[k]) when
  * dir[k] = 0, receive (from peer[k]) when dir[k] = 1; all complete on return. */
 MCEIK_HIDDEN int mceik_mpi_exchange_double(int fcomm, int nmsg, const int *dir, const int *peer, const int *tag,
@@ -247,4 +284,11 @@ MCEIK_HIDDEN int mceik_mpi_bcast_bytes(int fcomm, void *v, long long nbytes, int
     return -1;
 }
 MCEIK_HIDDEN int mceik_mpi_barrier(int fcomm) { (void)fcomm; return -1; }
+MCEIK_HIDDEN int mceik_mpi_comm_dup(int fcomm, int *fout) { (void)fcomm; (void)fout; return -1; }
+MCEIK_HIDDEN int mceik_mpi_comm_split(int fcomm, int color, int key, int *fout)
+{
+    (void)fcomm; (void)color; (void)key; (void)fout;
+    return -1;
+}
+MCEIK_HIDDEN int mceik_mpi_comm_free(int fcomm) { (void)fcomm; return -1; }
 #endif

@@ -17,6 +17,9 @@ MCEIK_HIDDEN int mceik_mpi_gather_bytes(int fcomm, const void *mine, void *all, 
 MCEIK_HIDDEN int mceik_mpi_scatter_bytes(int fcomm, const void *all, void *mine, long long nbytes, int root);
 MCEIK_HIDDEN int mceik_mpi_bcast_bytes(int fcomm, void *v, long long nbytes, int root);
 MCEIK_HIDDEN int mceik_mpi_barrier(int fcomm);
+MCEIK_HIDDEN int mceik_mpi_comm_dup(int fcomm, int *fout);
+MCEIK_HIDDEN int mceik_mpi_comm_split(int fcomm, int color, int key, int *fout);
+MCEIK_HIDDEN int mceik_mpi_comm_free(int fcomm);
 #ifdef __cplusplus
 }
 #endif

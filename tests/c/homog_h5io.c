@@ -4,11 +4,14 @@
  * broadcast_catalog hand them to every rank, each rank takes its block of the
  * grid (ndivx = ranks, homog.c:264-287), eikonal_h5io_initTTables creates the
  * table file, every table (one per lhasP / lhasS flag, homog.c:311-335) is
- * computed, written, read back and checked to 1e-5 (homog.c:340-415), then
+ * computed, written, read back and checked to 1e-5 (homog.c:340-415) -- the
+ * communicators from mpiutils_initialize3d / getCommunicators as homog.c
+ * builds them (homog.c:90-110) -- then
  * eikonal_h5io_initLocations, a logJPDF write / read, readModel,
  * getModelDimensions and finalize.  Exit 0 when every check passes.
  *
- *   mpiexec -n {1,2} homog_h5io <dir> <proj>
+ *   mpiexec -n {1,2,4} homog_h5io <dir> <proj> [ndivx]   (ndivx blocks per table: nprocs / ndivx
+ *   table groups, each writing <proj>_<group>_ttimes.h5 through its intra-table communicator)
  */
 #include <math.h>
 #include <stdio.h>
@@ -20,6 +23,7 @@
 #include "h5io.h"
 #include "mceik_broadcast.h"
 #include "mceik_struct.h"
+#include "mpiutils.h"
 
 #define CHECK(cond, ...)                                                    \
     do {                                                                    \
@@ -57,7 +61,24 @@ int main(int argc, char **argv)
     const double x0 = 0.0, y0 = 0.0, z0 = 0.0, x1 = 31.e3, y1 = 28.e3, z1 = 25.e3, dx = 1000., dy = 1000., dz = 1000.;
     const int nx = (int)((x1 - x0) / dx + 0.5) + 1, ny = (int)((y1 - y0) / dy + 0.5) + 1,
               nz = (int)((z1 - z0) / dz + 0.5) + 1;
-    const int nmodels = 1, model = 1, ndivx = nprocs, ndivy = 1, ndivz = 1;
+    const int nmodels = 1, model = 1, ndivx = argc > 3 ? atoi(argv[3]) : nprocs, ndivy = 1, ndivz = 1;
+    /* the table / block communicators (homog.c:90-110) */
+    int gcomm, intra, inter, ireord = 1, iwt = 0, ierr = 0;
+    const int world = (int)MPI_Comm_c2f(MPI_COMM_WORLD);
+    mpiutils_initialize3d(&world, &ireord, &iwt, &ndivx, &ndivy, &ndivz, &ierr);
+    CHECK(ierr == 0, "mpiutils_initialize3d");
+    mpiutils_getCommunicators(&gcomm, &intra, &inter, &ierr);
+    CHECK(ierr == 0, "mpiutils_getCommunicators");
+    const MPI_Comm intraComm = MPI_Comm_f2c((MPI_Fint)intra), interComm = MPI_Comm_f2c((MPI_Fint)inter);
+    int myblock = 0, mytable = 0, nblk = 0, ntab = 0;
+    MPI_Comm_rank(intraComm, &myblock);
+    MPI_Comm_rank(interComm, &mytable);
+    MPI_Comm_size(intraComm, &nblk);
+    MPI_Comm_size(interComm, &ntab);
+    CHECK(nblk == ndivx && ntab == nprocs / ndivx && myblock == myid % ndivx && mytable == myid / ndivx,
+          "communicator layout");
+    char tproj[256];
+    snprintf(tproj, sizeof(tproj), "%s_%d", proj, mytable + 1);   /* one table file per table group (homog.c:290-293) */
     struct mceik_stations_struct st;
     struct mceik_catalog_struct cat;
     memset(&st, 0, sizeof(st));
@@ -121,8 +142,10 @@ int main(int argc, char **argv)
     CHECK(!strcmp(st.stnm[5], "RC6") && !strcmp(st.chan[0], "HH?") && st.lhasS[2] == 0 && st.lhasS[3] == 1,
           "broadcast station fields");
     CHECK(cat.pickType[1] == S_PRIMARY_PICK && cat.statPtr[47] == 6 && cat.varObs[17] == 0.25, "broadcast catalog");
-    /* this rank's block (homog.c:264-287, mpiutils' rank -> x-fastest block) */
-    const int imbx = myid % ndivx, imby = (myid / ndivx) % ndivy, imbz = myid / (ndivx * ndivy);
+    /* this rank's block (homog.c:264-287) */
+    int imbx, imby, imbz, e = 0;
+    mpiutils_grd2ijk(&myblock, &ndivx, &ndivy, &ndivz, &imbx, &imby, &imbz, &e);
+    CHECK(e == 0, "grd2ijk");
     const int ndx = nx / ndivx > 1 ? nx / ndivx : 1, ndy = ny / ndivy > 1 ? ny / ndivy : 1,
               ndz = nz / ndivz > 1 ? nz / ndivz : 1;
     const int ix0 = imbx * ndx, iy0 = imby * ndy, iz0 = imbz * ndz;
@@ -131,8 +154,8 @@ int main(int argc, char **argv)
     const int nxL = ix1 - ix0, nyL = iy1 - iy0, nzL = iz1 - iz0;
     const size_t nloc = (size_t)nxL * nyL * nzL;
     hid_t tfid = -1, lfid = -1;
-    int ierr = eikonal_h5io_initTTables(MPI_COMM_WORLD, dir, proj, ix0, iy0, iz0, nx, ny, nz, nxL, nyL, nzL, nmodels,
-                                        st.nstat, false, x0, y0, z0, dx, dy, dz, &tfid);
+    ierr = eikonal_h5io_initTTables(intraComm, dir, tproj, ix0, iy0, iz0, nx, ny, nz, nxL, nyL, nzL, nmodels,
+                                    st.nstat, false, x0, y0, z0, dx, dy, dz, &tfid);
     CHECK(ierr == 0, "initTTables");
     double *tt = calloc(nloc, sizeof(double));
     float *t4 = calloc(nloc, sizeof(float));
@@ -145,11 +168,11 @@ int main(int argc, char **argv)
                               st.yrec[k], st.zrec[k], ph == S_PRIMARY_PICK ? vs : vp, tt);
             for (size_t i = 0; i < nloc; i++) t4[i] = (float)tt[i];
             /* homog.c:377 passes the 1-based table station number (k + 1 here) */
-            ierr = eikonal_h5io_writeTravelTimes(MPI_COMM_WORLD, tfid, k + 1, model, ph, ix0, iy0, iz0, nxL, nyL,
+            ierr = eikonal_h5io_writeTravelTimes(intraComm, tfid, k + 1, model, ph, ix0, iy0, iz0, nxL, nyL,
                                                  nzL, t4);
             CHECK(ierr == 0, "writeTravelTimes station %d phase %d", k + 1, ph);
             memset(t4, 0, nloc * sizeof(float));
-            ierr = eikonal_h5io_readTravelTimes(MPI_COMM_WORLD, tfid, k + 1, model, ph, ix0, iy0, iz0, nxL, nyL,
+            ierr = eikonal_h5io_readTravelTimes(intraComm, tfid, k + 1, model, ph, ix0, iy0, iz0, nxL, nyL,
                                                 nzL, t4);
             CHECK(ierr == 0, "readTravelTimes station %d phase %d", k + 1, ph);
             double dmax = 0.0;
@@ -158,13 +181,13 @@ int main(int argc, char **argv)
         }
     CHECK(ntables == 11, "table count %d", ntables);
     /* a missing dataset is an error on every rank */
-    CHECK(eikonal_h5io_readTravelTimes(MPI_COMM_WORLD, tfid, 7, model, 1, ix0, iy0, iz0, nxL, nyL, nzL, t4) != 0,
+    CHECK(eikonal_h5io_readTravelTimes(intraComm, tfid, 7, model, 1, ix0, iy0, iz0, nxL, nyL, nzL, t4) != 0,
           "station 7 does not exist");
     int gx = 0, gy = 0, gz = 0;
     CHECK(eikonal_h5io_getModelDimensions(tfid, &gx, &gy, &gz) == 0 && gx == nx && gy == ny && gz == nz,
           "getModelDimensions %d %d %d", gx, gy, gz);
     float *xl = calloc(nloc, sizeof(float)), *yl = calloc(nloc, sizeof(float)), *zl = calloc(nloc, sizeof(float));
-    CHECK(eikonal_h5io_readModel(MPI_COMM_WORLD, tfid, ix0, iy0, iz0, nxL, nyL, nzL, xl, yl, zl) == 0, "readModel");
+    CHECK(eikonal_h5io_readModel(intraComm, tfid, ix0, iy0, iz0, nxL, nyL, nzL, xl, yl, zl) == 0, "readModel");
     for (int k = 0; k < nzL; k++)
         for (int j = 0; j < nyL; j++)
             for (int i = 0; i < nxL; i++) {
@@ -175,13 +198,14 @@ int main(int argc, char **argv)
     ierr = eikonal_h5io_initLocations(MPI_COMM_WORLD, dir, proj, ix0, iy0, iz0, nx, ny, nz, nxL, nyL, nzL, nmodels,
                                       cat.nevents, x0, y0, z0, dx, dy, dz, &lfid);
     CHECK(ierr == 0, "initLocations");
-    for (size_t i = 0; i < nloc; i++) t4[i] = -(float)(i % 97) - 0.25f * (float)myid;
+    for (size_t i = 0; i < nloc; i++) t4[i] = -(float)(i % 97) - 0.25f * (float)myblock;
     CHECK(eikonal_h5io_writeLocationLogJPDF(MPI_COMM_WORLD, lfid, model, 2, ix0, iy0, iz0, nxL, nyL, nzL, t4) == 0,
           "writeLocationLogJPDF");
-    CHECK(eikonal_h5io_finalize(MPI_COMM_WORLD, &tfid) == 0 && eikonal_h5io_finalize(MPI_COMM_WORLD, &lfid) == 0,
+    CHECK(eikonal_h5io_finalize(intraComm, &tfid) == 0 && eikonal_h5io_finalize(intraComm, &lfid) == 0,
           "finalize");
+    mpiutils_finalize();
     MPI_Barrier(MPI_COMM_WORLD);
-    if (myid == 0) printf("homog_h5io: %d ranks, %d tables ok\n", nprocs, ntables);
+    if (myid == 0) printf("homog_h5io: %d ranks, %d table groups, %d tables ok\n", nprocs, ntab, ntables);
     MPI_Finalize();
     return 0;
 }

@@ -6,10 +6,12 @@ tests/c/homog_h5io.c restates homog.c:31-451's table and location I/O: rank
 / broadcast_catalog distribute them, every rank writes its block of each
 table (one per lhasP / lhasS flag) with eikonal_h5io_writeTravelTimes, reads
 it back and checks |d| <= 1e-5 (homog.c:389-413), then the location file.
-It must build against include/ and both libraries and pass under mpiexec -n
-1 and -n 2.  The files it leaves are then checked here dataset by dataset:
+The communicators come from mpiutils_initialize3d / getCommunicators as in
+homog.c:90-110 (table groups of ndivx blocks).  It must build against
+include/ and both libraries and pass under mpiexec -n 1, -n 2 and -n 4 (two
+table groups).  The files it leaves are then checked here dataset by dataset:
 with one rank they are bitwise what the serial Python writer (mceik_amd.h5io,
-the posterior writer's path) writes for the same tables; with two ranks they
+the posterior writer's path) writes for the same tables; with blocks they
 hold exactly what the reference's collective hyperslab writes leave (each
 rank's x-fastest block written through a {nxMax, nyMax, nzMax} memory space
 at {ix0, iy0, iz0}, h5io.c:883-925), restated here in numpy.
@@ -48,11 +50,12 @@ def homog_exe(tmp_path_factory):
     return exe
 
 
-def _run(exe, n, outdir):
-    r = subprocess.run([f"{MPI}/bin/mpiexec", "-n", str(n), exe, str(outdir), "homog"], capture_output=True,
-                       text=True, timeout=120)
+def _run(exe, n, outdir, ndivx=None):
+    ndivx = ndivx or n
+    r = subprocess.run([f"{MPI}/bin/mpiexec", "-n", str(n), exe, str(outdir), "homog", str(ndivx)],
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert f"homog_h5io: {n} ranks, 11 tables ok" in r.stdout
+    assert f"homog_h5io: {n} ranks, {n // ndivx} table groups, 11 tables ok" in r.stdout
     return r
 
 
@@ -119,7 +122,7 @@ def test_homog_flow_one_rank_equals_python_writer(homog_exe, tmp_path):
     loc = h5io.init_locations(str(py), "homog", NX, NY, NZ, 1, 4, 0.0, 0.0, 0.0, H, H, H)
     jp = -(np.arange(NX * NY * NZ) % 97).astype(np.float32)
     loc.write_logjpdf(1, 2, jp)
-    got = h5io.H5File.open(str(tmp_path / "homog_ttimes.h5"))
+    got = h5io.H5File.open(str(tmp_path / "homog_1_ttimes.h5"))
     try:
         assert got.dims() == (NX, NY, NZ)
         for a, b in zip(got.model(), ref.model()):
@@ -143,27 +146,31 @@ def test_homog_flow_one_rank_equals_python_writer(homog_exe, tmp_path):
         loc.close()
 
 
-def test_homog_flow_two_ranks_hyperslab_layout(homog_exe, tmp_path):
-    """mpiexec -n 2 (ndivx = 2, homog.c:82): the flow passes (broadcasts,
-    per-rank write / read-back within 1e-5, readModel of each block), and each
-    table dataset holds exactly the reference's collective hyperslab writes of
-    the two 16-node x blocks."""
-    _run(homog_exe, 2, tmp_path)
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_homog_flow_blocks_hyperslab_layout(homog_exe, tmp_path, nranks):
+    """mpiexec -n 2 and -n 4 with ndivx = 2 (homog.c:82): mpiutils_initialize3d
+    makes nranks / 2 table groups of two x blocks; the flow passes
+    (broadcasts, per-rank write / read-back within 1e-5, readModel of each
+    block), and each group's table file holds exactly the reference's
+    collective hyperslab writes of its two 16-node x blocks."""
+    _run(homog_exe, nranks, tmp_path, ndivx=2)
     nmax = (NX // 2, NY, NZ)
-    got = h5io.H5File.open(str(tmp_path / "homog_ttimes.h5"))
-    try:
-        for st, ph, x, y, z in _tables():
-            vel = VS if ph == 2 else VP
-            want = _hyperslab_file([(r * 16, _block_times(x, y, z, vel, r * 16, 16)) for r in range(2)], nmax)
-            name = h5io.travel_time_name(1, st, ph == 1)
-            assert np.array_equal(_raw(got, name).view(np.uint32), want.view(np.uint32)), name
-        k, j, i = np.meshgrid(np.arange(NZ), np.arange(NY), np.arange(16), indexing="ij")
-        xl = _hyperslab_file([(r * 16, ((r * 16 + i) * H).astype(np.float32).ravel()) for r in range(2)], nmax)
-        a = np.zeros(NX * NY * NZ, np.float32)
-        assert h5io.lib().mceik_h5io_readModel(got.fid, NX, NY, NZ, a.ctypes.data_as(C.c_void_p), None, None) == 0
-        assert np.array_equal(a, xl)
-    finally:
-        got.close()
+    for group in range(1, nranks // 2 + 1):
+        got = h5io.H5File.open(str(tmp_path / f"homog_{group}_ttimes.h5"))
+        try:
+            for st, ph, x, y, z in _tables():
+                vel = VS if ph == 2 else VP
+                want = _hyperslab_file([(r * 16, _block_times(x, y, z, vel, r * 16, 16)) for r in range(2)], nmax)
+                name = h5io.travel_time_name(1, st, ph == 1)
+                assert np.array_equal(_raw(got, name).view(np.uint32), want.view(np.uint32)), (group, name)
+            k, j, i = np.meshgrid(np.arange(NZ), np.arange(NY), np.arange(16), indexing="ij")
+            xl = _hyperslab_file([(r * 16, ((r * 16 + i) * H).astype(np.float32).ravel()) for r in range(2)], nmax)
+            a = np.zeros(NX * NY * NZ, np.float32)
+            assert h5io.lib().mceik_h5io_readModel(got.fid, NX, NY, NZ, a.ctypes.data_as(C.c_void_p), None,
+                                                   None) == 0
+            assert np.array_equal(a, xl)
+        finally:
+            got.close()
     gl = h5io.H5File.open(str(tmp_path / "homog_locations.h5"))
     try:
         blk = [(r * 16, (-(np.arange(16 * NY * NZ) % 97) - 0.25 * r).astype(np.float32)) for r in range(2)]
@@ -175,7 +182,7 @@ def test_homog_flow_two_ranks_hyperslab_layout(homog_exe, tmp_path):
 
 def test_reference_signature_exports():
     """Every function include/h5io.h declares is exported by libmceik_h5io.so,
-    and mceik_broadcast.h's by libmceik_hip.so."""
+    and mceik_broadcast.h's and mpiutils.h's by libmceik_hip.so."""
     def declared(h):
         txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", h)).read(), flags=re.S)
         return {m.group(1) for m in re.finditer(r"^\s*(?:int|void)\s+([A-Za-z_]\w*)\s*\(", txt, flags=re.M)}
@@ -185,6 +192,8 @@ def test_reference_signature_exports():
         return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     d = declared("h5io.h")
     assert len(d) == 15 and d <= exported(h5io.LIB_PATH), d - exported(h5io.LIB_PATH)
+    hip = exported(os.path.join(ROOT, "mceik_amd", "libmceik_hip.so"))
     b = declared("mceik_broadcast.h")
-    assert b == {"broadcast_stations", "broadcast_catalog"}
-    assert b <= exported(os.path.join(ROOT, "mceik_amd", "libmceik_hip.so"))
+    assert b == {"broadcast_stations", "broadcast_catalog"} and b <= hip
+    m = declared("mpiutils.h")
+    assert len(m) == 5 and m <= hip, m - hip
