@@ -238,6 +238,8 @@ def main():
     ap.add_argument("--raw-stats", action="store_true", help="add the raw FSM visit counters to the line")
     ap.add_argument("--precision", type=int, default=32, choices=(32, 64),
                     help="FSM arithmetic (64: the reference's literal fp64 update; tables fp32 either way)")
+    ap.add_argument("--max-waves", type=int, default=0,
+                    help="cap on the resident FSM waves per launch (0 = occupancy x CUs; experiments)")
     ap.add_argument("--f64-steps", type=int, default=2,
                     help="timed steps of the appended fp64 record (one GPU, --precision 32 runs; 0 = none)")
     ap.add_argument("--f64-warmup", type=int, default=1)
@@ -293,7 +295,7 @@ def main():
     p.var[:] = args.sigma ** 2
     p.nburn, p.keepk = args.warmup, max(1, args.steps)
     smp = mcmc.Sampler(p, nchains=hi - lo, chain_offset=lo, v0=v0, max_samples=1, device=local_rank,
-                       precision=args.precision)
+                       precision=args.precision, max_waves=args.max_waves)
     stream = torch.cuda.current_stream(dev)
     smp.set_stream(stream.cuda_stream)
 

@@ -235,9 +235,14 @@ __device__ __forceinline__ double sqrt_normal_f64(double x)
     return __builtin_fma(d, h, g);
 }
 
+#ifndef MCEIK_F64_NOBRANCH
+#define MCEIK_F64_NOBRANCH 0     // 1: the fast fp64 update as straight-line code (A/B)
+#endif
 // The literal fp64 update for the fast path (no ierr): godunov_sel's values
 // with the sort and the minima as bare v_min_f64 / v_max_f64, the 2D root
-// computed unconditionally (no divergent branch), and (FAST) the short sqrt.
+// computed unconditionally and no early return (no divergent branch: the
+// node updates of a brick form one basic block, so the scheduler can overlap
+// the next node's LDS neighbour reads), and (FAST) the short sqrt.
 // min(a1, a2) + f of the 2D fallback is x1 (a1 <= a2 by the sort).
 template <bool FAST>
 __device__ __forceinline__ double godunov_fast64(double a, double b, double c, double f)
@@ -254,8 +259,20 @@ __device__ __forceinline__ double godunov_fast64(double a, double b, double c, d
     const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
     const double disc = qb * qb - 4.0 * qc;
     const double x3 = 0.5 * (-qb + (FAST ? sqrt_normal_f64(disc) : __builtin_sqrt(disc)));
-    const bool r1 = !(x1 > a2), r2 = !(x2 > a3), nan_in = a1 == UN;
-    return nan_in ? UN : r1 ? x1 : r2 ? x2 : (x3 < UN ? x3 : UN);
+    // (a1 == UN needs no test of its own: then a2 = UN too, x1 = UN + f rounds
+    // to UN and the 1D case returns it -- the reference's early return)
+    const bool r1 = !(x1 > a2), r2 = !(x2 > a3);
+#if MCEIK_F64_NOBRANCH
+    // the choice as masks on the bit patterns: no ternary for the optimiser to
+    // turn into exec-masked branches (with the 2D / 3D arithmetic sunk into
+    // them); instcombine folds each mask pair back into one select
+    const unsigned long long m1 = 0ull - (unsigned long long)r1, m2 = 0ull - (unsigned long long)r2;
+    const unsigned long long b3 = __builtin_bit_cast(unsigned long long, dmin_(x3, UN));
+    const unsigned long long b23 = (__builtin_bit_cast(unsigned long long, x2) & m2) | (b3 & ~m2);
+    return __builtin_bit_cast(double, (__builtin_bit_cast(unsigned long long, x1) & m1) | (b23 & ~m1));
+#else
+    return r1 ? x1 : r2 ? x2 : (x3 < UN ? x3 : UN);
+#endif
 }
 
 // Branchless fp32 Godunov update, values and ierr identical to the twin

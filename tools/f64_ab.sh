@@ -1,11 +1,21 @@
+# fp64 sampler instance A/B on one box: each variant's libmceik_hip.so (mceik_amd/exp/lib_<v>.so;
+# v:N caps the resident waves at N) runs the C3 --precision 64 one-pipe bench twice, interleaved;
+# then the fp64 parity tests on variant F64_TEST
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/${F64_OUT:-f64e}
+O=gpurun_out/${F64_OUT:-f64e}
+mkdir -p $O
 cp mceik_amd/libmceik_hip.so /tmp/keep.so
-timeout -k 10 300 python -u -m pytest tests/test_gpu_fsm.py -x -q --timeout 250 --timeout-method thread -k "fp64 or inversion" > gpurun_out/${F64_OUT:-f64e}/tests.log 2>&1
-for r in 1 2; do for v in ${F64_VARIANTS:-f64br f64sel}; do
+for r in 1 2; do for vv in ${F64_VARIANTS:-f64a f64b f64c}; do
+  v=${vv%%:*}; mw=0; [ "$v" != "$vv" ] && mw=${vv#*:}
   cp mceik_amd/exp/lib_$v.so mceik_amd/libmceik_hip.so
-  timeout -k 10 300 python3 bench.py --precision 64 --steps 1 --warmup 1 --no-cpu-baseline --pipes 1 > gpurun_out/${F64_OUT:-f64e}/${v}_$r.log 2>&1
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" gpurun_out/${F64_OUT:-f64e}/${v}_$r.log $v | tee -a gpurun_out/${F64_OUT:-f64e}/summary.txt
+  timeout -k 10 300 python3 bench.py --precision 64 --steps 1 --warmup 1 --no-cpu-baseline --pipes 1 --max-waves $mw \
+      > $O/${v}_mw${mw}_$r.log 2>&1
+  v=${v}_mw$mw
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" $O/${v}_$r.log $v | tee -a $O/summary.txt
 done; done
+if [ -n "${F64_TEST:-}" ]; then
+  cp mceik_amd/exp/lib_$F64_TEST.so mceik_amd/libmceik_hip.so
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fsm.py tests/test_gpu_dropin.py -x -q --timeout 300 --timeout-method thread -k "fp64 or f64 or double or inversion or serial or reference" > $O/tests_$F64_TEST.log 2>&1
+fi
 cp /tmp/keep.so mceik_amd/libmceik_hip.so
