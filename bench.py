@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v30"          # bump when the sweep kernel changes; profiles/traffic.json must match
+KERNEL_REV = "fsm-v31"          # bump when the sweep kernel changes; profiles/traffic.json must match
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -141,7 +141,7 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config):
     kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
              "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)"
              if precision == 32 else "fsm_solve_kernel<double, 2, true, 2, 1, 4> (8-z steps, fp64 literal update, "
-                                     "short sqrt)")
+                                     "short sqrt, whole-line own loads)")
     # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
     # inputs did not change since their last visit are skipped)
     nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)

@@ -108,7 +108,13 @@ static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b
 //  9 neighbour rows XR, 10 neighbour rows XN: [2 halves][80 rows][4] R each -- row l < 64 holds lane l's
 //    8 z values (XR: its results of the last step, XN: its next brick), rows 64..79 the tile's halo columns |
 //  11 column info [nr][64] uint2 {own column offset, flags | tz | cell-cache base}
+//    (fp64 with MCEIK_F64_FL: XN is followed by HOLD [2][64] x 16 B, the held later halves of
+//    the whole-line own loads, fsm_kernel.hip line_issue64)
 #define MCEIK_CC_MAX 256         // cell-cache floats per position, upper bound
+#ifndef MCEIK_F64_FL
+#define MCEIK_F64_FL 1           // fp64 compile-time-kb instances: whole-line own loads
+#endif
+#define MCEIK_F64_HOLD (2 * 64 * 16)
 #define MCEIK_SMEM_ARRAYS 12
 #define MCEIK_XROWS 80           // neighbour-row array: 64 lanes + 8 x-halo + 8 y-halo rows
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -154,7 +160,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[7] = o; o += MCEIK_SCRATCH_BYTES;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 2 * MCEIK_XROWS * 4 * es;
-    off[10] = o; o += 2 * MCEIK_XROWS * 4 * es;
+    off[10] = o; o += 2 * MCEIK_XROWS * 4 * es + (es == 8 && MCEIK_F64_FL ? MCEIK_F64_HOLD : 0);
     off[11] = o; o += nr * 64 * 8;
     return o;
 }

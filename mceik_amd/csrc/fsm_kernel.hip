@@ -84,6 +84,8 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
 struct BInfo {
     uint32_t seg;            // byte offset (u buffer) of the own segment (OOB if none)
     uint32_t zh;             // the z-upwind node of a run start (prefetch only)
+    uint32_t lseg;           // this brick's half of its column line if the line holds a valid brick
+                             // (FL64 prefetch only: a loader whose own brick is past the grid end)
     int zb8, fl, ccb, ri;    // fl: C_* | F_*; ccb: cell-cache index of the brick (SLOWMODE 2); ri: ring slot
     int bid;                 // z-block id (stamps)
     int clk;                 // stream position of the brick (stamps)
@@ -101,6 +103,7 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Sm
     const bool valid = pos_valid(p, nstream) && (meta & C_BLK) && zb < L.nzb;
     const uint32_t zoff = zoff_bytes<R>(zb);
     b.seg = valid ? ci.x + zoff : OOB;
+    b.lseg = pos_valid(p, nstream) && (meta & C_BLK) && (zb & ~1) < L.nzb ? ci.x + zoff : OOB;
     const int zu = RZ ? zb * 8 + 8 : zb * 8 - 1;             // z-upwind node of the brick's first slot
     b.zh = (valid && (meta & C_ZH) && p.zbs == 0)
                ? ci.x + zoff_bytes<R>(zu >> 3) + (uint32_t)(zu & 7) * (uint32_t)sizeof(R) : OOB;
@@ -232,6 +235,57 @@ __device__ __forceinline__ void pair_store(Rsrc r, uint32_t seg, bool chg, const
     // (branch-free selects: both instructions carry all 64 lanes)
     bstore4(r, odd ? oth + 16u : own, odd ? x[0] : v[0], odd ? x[1] : v[1], odd ? x[2] : v[2], odd ? x[3] : v[3]);
     bstore4(r, odd ? own + 16u : oth, odd ? v[4] : x[0], odd ? v[5] : x[1], odd ? v[6] : x[2], odd ? v[7] : x[3]);
+}
+
+// ---- FL64: whole-line own loads of the fp64 compile-time-kb instances
+// (MCEIK_F64_FL).  A 128-B column line holds two 8-z fp64 bricks, which a
+// lane visits in two consecutive steps (kb even: a position's bricks pair up
+// as zbs 0/1, 2/3 in either z direction).  x-adjacent lanes (a pair) run one
+// step apart, so at every step exactly one lane of a pair -- the loader,
+// whose prefetch target is the first brick of a line in sweep order --
+// starts a line.  Both lanes load the loader's whole line in 4 dwordx4 loads
+// (lane parity p: quarters p and p + 2 of each half, so an instruction
+// touches 32 lines, 32 B of each): the now half goes to the loader's XN row
+// at the end of the step; the later half waits one step in LDS (HOLD) and
+// then goes to the row of the same lane, the non-loader of the next step.
+// As fsm16's FL, with the held half in LDS instead of registers (this
+// instance runs at its VGPR limit).  Without it a line was read as two 64-B
+// halves a step apart and the L2 re-fetched part of them in between.
+#ifndef MCEIK_ROTATE
+#define MCEIK_ROTATE 0
+#endif
+#define XHOLD(k) (XROW(2, 0, 0) + (k) * 128)         // HOLD quarter k of lane l: 2 values at + 2 l
+__device__ __forceinline__ void line_issue64(Rsrc r, uint32_t lseg, bool isl, double (&a)[4], double (&h)[4],
+                                             int &rowl, int &rowo)
+{
+    const int lane = threadIdx.x, par = lane & 1;
+    const bool islp = dpp_swap_pair((unsigned)isl) != 0u;
+    const uint32_t segp = dpp_swap_pair(lseg);
+    const uint32_t sl = isl ? lseg : (islp ? segp : OOB);     // the loader's now half
+    const uint32_t sh = sl ^ 64u;                             // its later half (OOB stays OOB)
+    const uint32_t o = (uint32_t)par * 16u;
+    d2v x = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, sl + o, 0, 0));
+    d2v y = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, sl + o + 32u, 0, 0));
+    d2v z = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, sh + o, 0, 0));
+    d2v w = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, sh + o + 32u, 0, 0));
+    a[0] = x.x; a[1] = x.y; a[2] = y.x; a[3] = y.y;
+    h[0] = z.x; h[1] = z.y; h[2] = w.x; h[3] = w.y;
+    rowl = isl ? lane : (lane ^ 1);
+    rowo = lane ^ (rowl == lane ? 1 : 0);
+}
+// end of step: the loader's next brick (this step's now half) and the other
+// lane's (the half held since the previous step) into the XN rows; this
+// step's later half into HOLD.  Quarter q of a row: half q >> 1, values
+// 2 (q & 1) .. + 1.
+__device__ __forceinline__ void line_write64(double *x, int rowl, int rowo, const double (&a)[4], const double (&h)[4])
+{
+    const int lane = threadIdx.x, par = lane & 1;
+    double *hd = x + XHOLD(0) + 2 * lane;
+    const double p0 = hd[0], p1 = hd[1], p2 = hd[128], p3 = hd[129];
+    hd[0] = h[0]; hd[1] = h[1]; hd[128] = h[2]; hd[129] = h[3];
+    double *l = x + XROW(1, 0, rowl) + 2 * par, *o = x + XROW(1, 0, rowo) + 2 * par;
+    l[0] = a[0]; l[1] = a[1]; l[4 * MCEIK_XROWS] = a[2]; l[4 * MCEIK_XROWS + 1] = a[3];
+    o[0] = p0; o[1] = p1; o[4 * MCEIK_XROWS] = p2; o[4 * MCEIK_XROWS + 1] = p3;
 }
 
 // Slowness of the 8 nodes of a segment (prefetch; multiplied by h when staged).
@@ -561,6 +615,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     R c[8], n[8], q[8], p[8], r[8], fq[8], hq[4], hn[4];
     constexpr bool PAIR = MCEIK_PAIR_LOAD && sizeof(R) == 4 && MCEIK_AHEAD == 2;
+    // FL64: whole-line own loads (line_issue64): la / lh this step's quarters
+    // of the loader's now / later half, rowl / rowo the XN rows they go to
+    constexpr bool FL64 = MCEIK_F64_FL && sizeof(R) == 8 && KB > 0 && (KB & 1) == 0 && MCEIK_AHEAD == 2 &&
+                          !MCEIK_ROTATE;
+    double la[4], lh[4];
+    int rowl = 0, rowo = 0;
     float qa[4], qb[4];                  // PAIR: raw halves of q
     R zc, zn, zq, zp;                // z-upwind values of run starts (vb .. vb+3)
     float ccv[CCR];
@@ -636,6 +696,24 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     store4(S.xr + hso, hq);                       // halos of vb0
     store_row(S.xr, 0, lane, r);                   // no results yet (u_nan)
     store_row(S.xr, 1, lane, n);                   // brick vb0 + 1
+    if (FL64) {
+        // HOLD for step 0: quarters p, p + 2 of the brick the pair's step-0
+        // non-loader targets (the second brick of a line it would have started
+        // one step earlier), loaded from that lane's own segment
+        Pos pn = p3;
+        pos_adv(pn, kb, nr);
+        const bool nl = pn.vb >= 0 && (pn.zbs & 1) == 1;
+        const uint32_t sn = nl ? brick_info<R, RZ, ZSH>(L, kb, S, pn, nstream, lx, ly, bc,
+                                                         S.cinfo[pn.ri * 64 + lane]).seg
+                               : OOB;
+        const bool nlp = dpp_swap_pair((unsigned)nl) != 0u;
+        const uint32_t snp = dpp_swap_pair(sn);
+        const uint32_t s0 = (nl ? sn : (nlp ? snp : OOB)) + (uint32_t)(lane & 1) * 16u;
+        d2v x = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(ur, s0, 0, 0));
+        d2v y = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(ur, s0 + 32u, 0, 0));
+        double *hd = reinterpret_cast<double *>(S.xr) + XHOLD(0) + 2 * lane;
+        hd[0] = x.x; hd[1] = x.y; hd[128] = y.x; hd[129] = y.y;
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) hq[i] = hn[i];
     // Wait for the prologue's loads here, once per sweep: a register the loop
@@ -724,6 +802,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         } else {
             if (PAIR)
                 pair_issue(ur, b3.seg, qa, qb);
+            else if (FL64)
+                line_issue64(ur, b3.lseg, p3.vb >= 0 && (p3.zbs & 1) == 0, la, lh, rowl, rowo);
             else
                 bload8(ur, b3.seg, q);
             zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
@@ -778,7 +858,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         } else {
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                nn[i] = q[i];
+                if (!FL64) nn[i] = q[i];
                 if (AH == 3) q[i] = p[i];
             }
         }
@@ -798,7 +878,10 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (LAZYN) u0_store();
         store_row(S.xr, 0, lane, r);
         if (LAZYN) load_row(S.xr, XROW(1, 0, lane), c);
-        store_row(S.xr, 1, lane, nn);
+        if (FL64)
+            line_write64(reinterpret_cast<double *>(S.xr), rowl, rowo, la, lh);
+        else
+            store_row(S.xr, 1, lane, nn);
         if (!ROT) {
 #pragma unroll
             for (int i = 0; i < 4; i++) hq[i] = hn[i];
@@ -808,7 +891,13 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         // materialise the copies here (the loads' waits land here, before the
         // stores); otherwise they become the loop's phi copies at the latch
 #pragma unroll
-        for (int i = 0; i < 8; i++) asm volatile("" : "+v"(nn[i]));
+        for (int i = 0; i < 8; i++) {
+            if (!FL64) asm volatile("" : "+v"(nn[i]));
+        }
+        if (FL64) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) asm volatile("" : "+v"(la[i]), "+v"(lh[i]));
+        }
         if (!ROT) asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]));
         asm volatile("" : "+v"(zn));
         asm volatile("" ::: "memory");

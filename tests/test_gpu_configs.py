@@ -105,6 +105,36 @@ def test_c3_bench_production_launch_bitwise():
 
 
 @pytest.mark.timeout(600)
+def test_c3_fp64_sampler_tables_bitwise():
+    """The bench line's f64 record: Sampler(C3, precision=64) launches the fp64
+    instance with the short sqrt (fsm_solve_kernel<double, 2, true, 2, 1, 4>).
+    Chain 0's initial tables of stations 0..5 == the fp64 oracle (bitwise the
+    reference on the goldens) on the expanded fp32 cell slowness, cast to
+    fp32; iteration counts equal."""
+    dev = _dev()
+    from mceik_amd import mcmc
+    p = _problem("C3")
+    s = mcmc.Sampler(p, nchains=1, precision=64)
+    assert s.info()["kernel"].startswith("fsm_solve_kernel<double, 2, true, 2, 1, 4>"), s.info()["kernel"]
+    v0, _, _, _ = s.state()
+    ttab, niter, _, ierr = s.last(with_ierr=True)
+    s.close()
+    assert not ierr.any()
+    scell = (1.0 / v0[0].astype(np.float32)).reshape(p.ncz, p.ncy, p.ncx)
+    k, j, i = np.meshgrid(np.arange(p.nz), np.arange(p.ny), np.arange(p.nx), indexing="ij")
+    sfield = scell[k // p.nrz, j // p.nry, i // p.nrx].ravel().astype(np.float64)
+    stations = range(6)
+    with cf.ThreadPoolExecutor(6) as ex:
+        res = list(ex.map(lambda st: O.eikonal_solve(p.nx, p.ny, p.nz, sfield, p.h,
+                                                     [(0.0, p.sx[st], p.sy[st], p.sz[st])], p.maxit, p.tol,
+                                                     p.x0, p.y0, p.z0), stations))
+    for st, (u, e, it) in zip(stations, res):
+        assert e == 0
+        assert np.array_equal(ttab[0, st].view(np.uint32), u[p.ev_node].astype(np.float32).view(np.uint32)), st
+        assert int(niter[0, st]) == it, st
+
+
+@pytest.mark.timeout(600)
 def test_c5_sampler_launch_bitwise():
     """C5 through the sampler: 256^3, 64 stations, 32 chains = 2048 solves per
     step on scratch-budget-capped waves (the runtime-kb fsm16 instance with

@@ -171,13 +171,15 @@ def test_fp64_batch_bitwise_vs_oracle(case):
     assert int(out["ierr"][0]) == ierr
 
 
-@pytest.mark.parametrize("nz,max_waves", [(34, 0), (67, 2)], ids=["kb4", "kb4_ragged_reuse"])
-def test_fp64_inversion_grid_mode_bitwise(nz, max_waves):
+@pytest.mark.parametrize("nz,max_waves,fast", [(34, 0, False), (34, 0, True), (67, 2, True)],
+                         ids=["kb4", "kb4_short_sqrt", "kb4_short_sqrt_ragged_reuse"])
+def test_fp64_inversion_grid_mode_bitwise(nz, max_waves, fast):
     """The fp64 sampler's kernel (bench.py --precision 64): per-cell fp32
     slowness, fp64 fields and the literal update.  Several models and stations
     per launch (max_waves 2: several solves per wave in reused scratch);
     fields, event tables, iterations bitwise = the fp64 oracle on the expanded
-    field."""
+    field.  fast=True is the instance the sampler launches (the short sqrt,
+    bare v_min/v_max_f64: fsm_update.h godunov_fast64)."""
     dev = _dev()
     nx, ny, h, nref = 30, 26, 100.0, (4, 4, 4)
     ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
@@ -190,7 +192,7 @@ def test_fp64_inversion_grid_mode_bitwise(nz, max_waves):
                     [[0.1, 1500.0, 1200.0, 1700.0]]])
     ev = rng.integers(0, nx * ny * nz, 7).astype(np.int32)
     from mceik_amd.eikonal import BatchSolver
-    bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 64, nref=nref)
+    bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 64, nref=nref, fast_sqrt=fast)
     out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(nmodel, -1), device=dev),
                    ev_node=torch.tensor(ev), want_fields=True, max_waves=max_waves)
     assert out["step_z"] == 8

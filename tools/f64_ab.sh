@@ -1,6 +1,6 @@
 # fp64 sampler instance A/B on one box: each variant's libmceik_hip.so (mceik_amd/exp/lib_<v>.so;
 # v:N caps the resident waves at N) runs the C3 --precision 64 one-pipe bench twice, interleaved;
-# then the fp64 parity tests on variant F64_TEST
+# then the fp64 parity tests on each variant in F64_TEST
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${F64_OUT:-f64e}
@@ -14,8 +14,10 @@ for r in 1 2; do for vv in ${F64_VARIANTS:-f64a f64b f64c}; do
   v=${v}_mw$mw
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" $O/${v}_$r.log $v | tee -a $O/summary.txt
 done; done
-if [ -n "${F64_TEST:-}" ]; then
-  cp mceik_amd/exp/lib_$F64_TEST.so mceik_amd/libmceik_hip.so
-  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fsm.py tests/test_gpu_dropin.py -x -q --timeout 300 --timeout-method thread -k "fp64 or f64 or double or inversion or serial or reference" > $O/tests_$F64_TEST.log 2>&1
-fi
+for t in ${F64_TEST:-}; do
+  cp mceik_amd/exp/lib_$t.so mceik_amd/libmceik_hip.so
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fsm.py tests/test_gpu_dropin.py tests/test_gpu_configs.py -x -q --timeout 300 --timeout-method thread -k "fp64 or f64 or double or inversion or serial or reference" > $O/tests_$t.log 2>&1 && rc=0 || rc=$?
+  echo "tests $t rc=$rc" | tee -a $O/summary.txt
+  [ $rc -le 1 ] || exit $rc                      # assertion failures only; a fault / abort / timeout ends the run
+done
 cp /tmp/keep.so mceik_amd/libmceik_hip.so

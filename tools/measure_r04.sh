@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # On the GPU box: the r04 evidence set for the current kernels.
 #  1 rocprofv3 kernel-trace stats of the default bench (fp32 two pipes + the fp64 record)
-#  2 fp32, one pipe, the timed launch: raw visit counters, PMC FETCH_SIZE; WRITE_SIZE; SQ
+#  2 fp32, one pipe, the timed launch: raw visit counters, PMC FETCH_SIZE; WRITE_SIZE; SQ; SQ issue + clock
 #  3 fp64 (--precision 64), one pipe: the same
 #  4 the N = 2 flow rehearsed on one GPU (MCEIK_BENCH_REHEARSAL=1, gloo)
 # Outputs under gpurun_out/${M_OUT:-m04}/.  Every step under its own time limit.
@@ -13,6 +13,8 @@ mkdir -p "$O"
 HB=$!
 trap 'kill $HB 2>/dev/null || true' EXIT
 SQ="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES"
+# issue breakdown (quad-cycles summed over waves) + the effective clock (GRBM_GUI_ACTIVE / 8 / launch time)
+SQ2="SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
 echo "[measure_r04] trace"
 timeout -k 10 480 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --f64-steps 2 > "$O/bench_under_trace.log" 2>&1
@@ -22,7 +24,7 @@ for prec in 32 64; do
   timeout -k 10 300 python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --pipes 1 --raw-stats --precision $prec \
       > "$O/bench_f${prec}_pipes1_raw.log" 2>&1
   i=0
-  for P in FETCH_SIZE WRITE_SIZE "$SQ"; do
+  for P in FETCH_SIZE WRITE_SIZE "$SQ" "$SQ2"; do
     i=$((i+1))
     echo "[measure_r04] fp$prec pmc$i"
     timeout -k 10 400 rocprofv3 --pmc $P --kernel-include-regex "$K" -d "$O/f${prec}_pmc$i" -o pmc \

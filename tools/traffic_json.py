@@ -32,6 +32,14 @@ def record(d, prec, rev, rnd):
     f1, n1 = pmc(os.path.join(d, f"f{prec}_pmc1"), match)
     f2, n2 = pmc(os.path.join(d, f"f{prec}_pmc2"), match)
     sq, _ = pmc(os.path.join(d, f"f{prec}_pmc3"), match)
+    iss, clk = {}, None
+    if os.path.isdir(os.path.join(d, f"f{prec}_pmc4")):
+        iss, _ = pmc(os.path.join(d, f"f{prec}_pmc4"), match)
+        l4 = [x for x in open(os.path.join(d, f"bench_f{prec}_pmc4.log")) if x.startswith("{")][-1]
+        ms4 = json.loads(l4)["roofline"]["avg_launch_ms"]
+        if "GRBM_GUI_ACTIVE" in iss:
+            clk = round(iss.pop("GRBM_GUI_ACTIVE") / 8.0 / (ms4 * 1e-3) / 1e9, 3)
+        iss.pop("GRBM_COUNT", None)
     line = json.loads(open(os.path.join(d, f"bench_f{prec}_pipes1_raw.log")).read().strip().splitlines()[-1])
     ws = line["roofline"]["wave_steps_per_step"]
     fetch = f1["FETCH_SIZE"] * 1024.0
@@ -54,6 +62,8 @@ def record(d, prec, rev, rnd):
         "source": f"tools/measure_r04.sh ({d}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ passes over bench.py "
                   f"--steps 1 --warmup 1 --pipes 1 --precision {prec}, {match} dispatches averaged)",
         "sq_per_launch": {k: v for k, v in sorted(sq.items())},
+        "sq_issue_per_launch": {k: v for k, v in sorted(iss.items())} or None,
+        "effective_clock_ghz": clk,
         "wave_steps_per_launch": int(ws),
         "valu_per_wave_step": round(sq["SQ_INSTS_VALU"] / ws, 1) if "SQ_INSTS_VALU" in sq else None,
         "z_per_wave_step": 16 if prec == 32 else 8,
