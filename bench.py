@@ -27,7 +27,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
-KERNEL_REV = "fsm-v31"          # bump when the sweep kernel changes; profiles/traffic.json must match
+# sweep-kernel revision per precision (bump when that kernel changes; the
+# profiles/traffic.json record of that precision must match)
+KERNEL_REVS = {32: "fsm-v31", 64: "fsm-v32"}
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -141,7 +143,7 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config):
     kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
              "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)"
              if precision == 32 else "fsm_solve_kernel<double, 2, true, 2, 1, 4> (8-z steps, fp64 literal update, "
-                                     "short sqrt, whole-line own loads)")
+                                     "short sqrt, whole-line own loads, compact LDS: 8 waves/CU)")
     # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
     # inputs did not change since their last visit are skipped)
     nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
@@ -169,14 +171,14 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config):
             tj = json.load(f)
         rec = tj.get("f64", {}) if precision == 64 else tj
         if (rec.get("workload") == config and rec.get("chains_per_gpu") == per_gpu
-                and rec.get("kernel_rev") == KERNEL_REV):
+                and rec.get("kernel_rev") == KERNEL_REVS[precision]):
             traffic = rec.get("hbm_bytes_per_launch")     # one single-pipe launch = one step
-            traffic_src = (f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of kernel_rev {KERNEL_REV} "
+            traffic_src = (f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of kernel_rev {KERNEL_REVS[precision]} "
                            f"({rec.get('source', 'profiles/traffic.json')}); not measured in this run")
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": kname,
-            "kernel_rev": KERNEL_REV,
+            "kernel_rev": KERNEL_REVS[precision],
             "timing": (f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
                        if pipes > 1 else "HIP events around each FSM launch"),
             "per": "step: every per-unit field below is per step or per solve, whatever the pipes",

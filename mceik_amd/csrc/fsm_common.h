@@ -138,6 +138,16 @@ static inline __host__ __device__ bool fsm_fixed_layout(const FsmLaunch &L, size
     return es == 4 && L.slow_mode != 0 && L.cell_cache && L.fast_sqrt && L.nrz == 4 && L.ccb <= 64 &&
            L.kb == MCEIK_KB && L.nr == FSMF_NR && L.nblocks <= MCEIK_MAX_BLOCKS;
 }
+// The compact layout of the fp64 compile-time-kb instances (fsm_kernel.hip
+// variants 15, 16; Smem<R, true>): 16-bit block clocks rebased per iteration
+// (an iteration takes at most 8 (nblocks (1 + vis) + infl) + 64 < 2^16
+// clocks at nblocks <= MCEIK_MAX_BLOCKS, kb = MCEIK_KB), one meta word per
+// lane and position, the tile base per position in the ring.
+static inline __host__ __device__ bool fsm_compact_layout(const FsmLaunch &L, size_t es)
+{
+    return es == 8 && L.slow_mode != 0 && L.cell_cache && L.nrz == 4 && L.ccb <= 64 && L.kb == MCEIK_KB &&
+           L.nblocks <= MCEIK_MAX_BLOCKS;
+}
 static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, size_t es, size_t *off)
 {
     if (fsm_fixed_layout(L, es)) {
@@ -152,16 +162,17 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     size_t o = 0;
     off[0] = o; o += mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
     off[1] = o; o += cached ? mceik_align16(nr * L.ccb * 4) : 0;
+    const bool cmp = fsm_compact_layout(L, es);
     off[2] = o; o += mceik_align16(nt * 4);
-    off[3] = o; o += mceik_align16(nb * 4);
-    off[4] = o; o += mceik_align16(nb * 4);
+    off[3] = o; o += mceik_align16(nb * (cmp ? 2 : 4));
+    off[4] = o; o += mceik_align16(nb * (cmp ? 2 : 4));
     off[5] = o;
-    off[6] = o; o += mceik_align16(nr * 8);
+    off[6] = o; o += mceik_align16(nr * (cmp ? 12 : 8));
     off[7] = o; o += MCEIK_SCRATCH_BYTES;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 2 * MCEIK_XROWS * 4 * es;
     off[10] = o; o += 2 * MCEIK_XROWS * 4 * es + (es == 8 && MCEIK_F64_FL ? MCEIK_F64_HOLD : 0);
-    off[11] = o; o += nr * 64 * 8;
+    off[11] = o; o += nr * 64 * (cmp ? 4 : 8);
     return o;
 }
 static inline size_t fsm_lds_bytes(const FsmLaunch &L, size_t es)

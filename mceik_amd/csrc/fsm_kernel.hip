@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "fsm_common.h"
 #include "fsm_device.h"
 #include "fsm_update.h"
@@ -41,22 +43,29 @@ namespace {
 // decided, so a run never stops early).  Bubble positions keep an upwind x/y
 // neighbour's visit >= vis positions back (halo visibility).  Per-block
 // clocks live in LDS.
-template <typename R>
+// CMP (the compact layout, fsm_compact_layout(): the fp64 compile-time-kb
+// instances): 16-bit block clocks rebased at every iteration (iter_norm, as
+// fsm16_kernel.hip), and per position one meta word per lane plus the tile
+// base (ring) instead of {own column, meta} -- 25.4 -> 19.9 KB of LDS at C3,
+// 6 -> 8 resident waves per CU.
+template <typename R, bool CMP = false>
 struct Smem {
+    using clk_t = typename std::conditional<CMP, unsigned short, int>::type;
     int *box;                    // BC boxes [nsrc][6]
     float *cc;                   // cell cache [nr][ccb]                   (SLOWMODE 2)
     int *order;                  // diagonal tile order: txs | tys << 16   [ntiles]
-    int *lastproc, *lastchg;     // per z-block stream clock of the last visit / last visit with a change
+    clk_t *lastproc, *lastchg;   // per z-block stream clock of the last visit / last visit with a change
     int *ring;                   // per position (mod nr): block entry tx | ty << 12 | tz << 24, bubble -1;
-                                 // then [nr] the z-block ids
+                                 // then [nr] the z-block ids (CMP: then [nr] the tile base offsets)
     int *scratch;                // debug counters
     u2v *cinfo;                  // [nr][64] column info of every lane per position: {own column, meta}
+    unsigned *meta;              // CMP: [nr][64] the meta word only (own column = tile base + lane column)
     R *sf;                       // staged slowness*h (modes 0,1)
     R *xr;                       // neighbour rows: XR [2 halves][80 rows][4], then XN (same shape)
 };
 
-template <typename R, bool FIXED>
-__device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *base)
+template <typename R, bool FIXED, bool CMP>
+__device__ __forceinline__ Smem<R, CMP> smem_bind(const FsmLaunch &L, unsigned char *base)
 {
     size_t off[MCEIK_SMEM_ARRAYS];
     if (FIXED) {         // fsm_fixed_layout(): constants (the host checked the predicate)
@@ -66,18 +75,30 @@ __device__ __forceinline__ Smem<R> smem_bind(const FsmLaunch &L, unsigned char *
     } else {
         fsm_smem_layout(L, sizeof(R), off);
     }
-    Smem<R> S;
+    Smem<R, CMP> S;
     S.box = reinterpret_cast<int *>(base + off[0]);
     S.cc = reinterpret_cast<float *>(base + off[1]);
     S.order = reinterpret_cast<int *>(base + off[2]);
-    S.lastproc = reinterpret_cast<int *>(base + off[3]);
-    S.lastchg = reinterpret_cast<int *>(base + off[4]);
+    S.lastproc = reinterpret_cast<typename Smem<R, CMP>::clk_t *>(base + off[3]);
+    S.lastchg = reinterpret_cast<typename Smem<R, CMP>::clk_t *>(base + off[4]);
     S.ring = reinterpret_cast<int *>(base + off[6]);
     S.scratch = reinterpret_cast<int *>(base + off[7]);
     S.sf = reinterpret_cast<R *>(base + off[8]);
     S.xr = reinterpret_cast<R *>(base + off[9]);       // arrays 9 (XR) and 10 (XN) are contiguous
     S.cinfo = reinterpret_cast<u2v *>(base + off[11]);
+    S.meta = reinterpret_cast<unsigned *>(base + off[11]);
     return S;
+}
+// column info {own column, meta} of lane l at ring slot ri (col: lane l's
+// column offset inside its tile, used by the compact layout)
+template <typename R, bool CMP>
+__device__ __forceinline__ u2v cinfo_at(const FsmLaunch &L, const Smem<R, CMP> &S, int ri, int l, uint32_t col)
+{
+    if (!CMP) return S.cinfo[ri * 64 + l];
+    u2v c;
+    c.x = (uint32_t)S.ring[2 * L.nr + ri] + col;
+    c.y = S.meta[ri * 64 + l];
+    return c;
 }
 
 // What a lane needs about one of its bricks.
@@ -92,8 +113,8 @@ struct BInfo {
     int bcm;                 // BC z-slots of the segment (generic path)
 };
 
-template <typename R, bool RZ, int ZSH>
-__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Smem<R> &S, const Pos &p, int nstream,
+template <typename R, bool RZ, int ZSH, bool CMP>
+__device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Smem<R, CMP> &S, const Pos &p, int nstream,
                                             int lx, int ly, const BcBoxes &bc, const u2v ci)
 {
     BInfo b;
@@ -290,8 +311,8 @@ __device__ __forceinline__ void line_write64(double *x, int rowl, int rowo, cons
 
 // Slowness of the 8 nodes of a segment (prefetch; multiplied by h when staged).
 // Modes 0 and 1 only; the column's x, y come from the stream ring.
-template <typename R, int SLOWMODE>
-__device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R> &S, Rsrc sr, const BInfo &b,
+template <typename R, int SLOWMODE, bool CMP>
+__device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R, CMP> &S, Rsrc sr, const BInfo &b,
                                               int lx, int ly, R (&s)[8])
 {
     if (SLOWMODE == 0) {
@@ -322,8 +343,8 @@ __device__ __forceinline__ void prefetch_slow(const FsmLaunch &L, const Smem<R> 
 // would recompute every node from unchanged inputs and return the current
 // value.  Once a run starts, the next block's z-upwind neighbour is in flight,
 // so the run covers the rest of the column.
-template <typename R, bool RZ>
-__device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R> &S, Stream &st, int C, int rx, int ry, int &zh)
+template <typename R, bool RZ, bool CMP>
+__device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R, CMP> &S, Stream &st, int C, int rx, int ry, int &zh)
 {
     const int lane = threadIdx.x;
     const int nt = L.ntiles, nzk = L.nzk;
@@ -376,8 +397,8 @@ __device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R> &S, Stre
         for (int kz = st.k0 + lane; kz < nzk; kz += 64) {
             const int tz = RZ ? nzk - 1 - kz : kz;
             int p = -0x40000000;
-            if (txs > 0) p = max(p, S.lastproc[tz * nt + id + (rx ? 1 : -1)]);
-            if (tys > 0) p = max(p, S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)]);
+            if (txs > 0) p = max(p, (int)S.lastproc[tz * nt + id + (rx ? 1 : -1)]);
+            if (tys > 0) p = max(p, (int)S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)]);
             need = max(need, p + L.vis - (kz - st.k0) - C);
         }
         st.wait = __builtin_amdgcn_readfirstlane(wave_max(need));
@@ -419,19 +440,21 @@ __device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R> &S, Stre
 // ring entry, the block id and the block's clocks) or a bubble.  Visit
 // statistics: the bricks lane (0,0) will update (= z-bricks of the block in
 // the grid) and the column segments of all lanes (S.scratch[0], [1]).
-template <typename R>
-__device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> &S, const BcBoxes &bc, int entry,
+template <typename R, bool CMP>
+__device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R, CMP> &S, const BcBoxes &bc, int entry,
                                       int zh, int ri, int clock, int clock_it, int lx, int ly, int lxs, int lys, int rx,
                                       int ry, ColTile &ct)
 {
     u2v ci;
     int bid = 0, nbv = 0;
+    uint32_t tbase = 0;
     if (entry >= 0) {
         const int tz = (entry >> 24) & 0xff;
         bid = tz * L.ntiles + (entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx;
+        tbase = (uint32_t)((entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx) * tile_bytes<R>(L);
         nbv = min(kb, L.nzb - tz * kb);
         // first visit of the block in this iteration: no visit since the iteration's first clock
-        const int u0flag = S.lastproc[bid] < clock_it;
+        const int u0flag = (int)S.lastproc[bid] < clock_it;
         if ((entry & 0xffffff) != ct.tile) column_tile<R>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         ci.x = ct.col;
         ci.y = column_word(L, kb, ct, tz, ri, u0flag, zh);
@@ -440,10 +463,14 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> 
     }
     const int nact = L.visit_stats && entry >= 0 ? __builtin_popcountll(__ballot(ct.fl & C_ACT)) : 0;
     asm volatile("" ::: "memory");
-    S.cinfo[ri * 64 + threadIdx.x] = ci;
+    if (CMP)
+        S.meta[ri * 64 + threadIdx.x] = ci.y;
+    else
+        S.cinfo[ri * 64 + threadIdx.x] = ci;
     if (threadIdx.x == 0) {
+        if (CMP) S.ring[2 * L.nr + ri] = (int)tbase;
         if (entry >= 0) {
-            S.lastproc[bid] = clock;
+            S.lastproc[bid] = (typename Smem<R, CMP>::clk_t)clock;
             if (L.visit_stats) {
                 S.scratch[0] += nbv;
                 S.scratch[1] += nbv * nact;
@@ -458,8 +485,8 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R> 
 // x/y neighbour minima and f = s*h of slot pj.  The four neighbour rows
 // (x/y-upwind lanes' new values, downwind lanes' old values, or the halo
 // rows for tile-edge lanes) were read from LDS at the start of the brick.
-template <typename R, int SLOWMODE, int ZSH, bool GENERIC, bool WANTF>
-__device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, const R (&c)[8],
+template <typename R, int SLOWMODE, int ZSH, bool GENERIC, bool WANTF, bool CMP>
+__device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R, CMP> &S, const BInfo &b0, const R (&c)[8],
                                           const R (&xmr)[8], const R (&xpr)[8], const R (&ymr)[8], const R (&ypr)[8],
                                           int pj, bool xp, bool xn, bool yp, bool yn, R &ux, R &uy, R &fv)
 {
@@ -491,8 +518,8 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R> &S, 
 // ierr); otherwise the brick is interior to the grid in x, y and z up to the
 // sweep-order first/last brick, no lane holds a BC node, and every lane's
 // missing x/y neighbours are already its own old values (column_info).
-template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC>
-__device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &S, const BInfo &b0, R (&c)[8],
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC, bool CMP>
+__device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, CMP> &S, const BInfo &b0, R (&c)[8],
                                              R (&n)[8], R (&r)[8], R zc, int lx, int ly, int rx, int ry,
                                              bool &changed, bool &nc, int &ierr_last)
 {
@@ -592,9 +619,9 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R> &
 // KB > 0: the launch's kb (bricks per z-block) as a compile-time constant
 // (the ring then has nr = 2 + 16 / KB slots); 0: runtime L.kb / L.nr.
 // nchg: per-lane count of changed column segments (visit statistics).
-template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB>
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB, bool CMP>
 __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
-                                     const Smem<R> &S, int rx, int ry, int clock_it, int clock0,
+                                     const Smem<R, CMP> &S, int rx, int ry, int clock_it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
@@ -609,6 +636,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     const unsigned hbit = hj < 16 ? C_XOWN : C_YOWN;
     const uint32_t hdelta = halo_delta(L, tile_bytes<R>(L), hj, he, rx, ry);
     const int hso = halo_row_off(lane);
+    // column offsets inside a tile (the compact layout's cinfo_at): this lane's, the halo edge lane's
+    const uint32_t lanecol = (uint32_t)colpos(lx, ly) * 128u;
+    const uint32_t hcol = (uint32_t)colpos(rx ? 7 - (he & 7) : (he & 7), ry ? 7 - (he >> 3) : (he >> 3)) * 128u;
 
     // stream bookkeeping (wave-uniform)
     Stream st;
@@ -655,14 +685,14 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     // prefetch and carries it (one column-info read and decode per brick).
     Pos p3;
     pos_init(p3, -d, kb, nr);
-    BInfo b0 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
+    BInfo b0 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, cinfo_at(L, S, p3.ri, lane, lanecol));
     // prologue: c, n, q = bricks vb0 .. vb0+2; stage f and halos of vb0
     bload8(ur, b0.seg, c);
     if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b0, lx, ly, fq);
     Pos pe;                              // the halo's edge lane position (vb+2 in the loop)
     pos_init(pe, -hd, kb, nr);
     {
-        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, S.cinfo[pe.ri * 64 + he], hbit, hdelta);
+        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, cinfo_at(L, S, pe.ri, he, hcol), hbit, hdelta);
         bload4(ur, ho, hq);
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
@@ -670,11 +700,11 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     TRAF(S, 0, b0.seg != OOB, 8 * sizeof(R));
     TRAF(S, 2, b0.zh != OOB, sizeof(R));
     pos_adv(p3, kb, nr);
-    BInfo b1 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
+    BInfo b1 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, cinfo_at(L, S, p3.ri, lane, lanecol));
     bload8(ur, b1.seg, n);
     pos_adv(pe, kb, nr);
     {
-        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, S.cinfo[pe.ri * 64 + he], hbit, hdelta);
+        const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, cinfo_at(L, S, pe.ri, he, hcol), hbit, hdelta);
         bload4(ur, ho, hn);   // halos of vb+1
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
@@ -684,7 +714,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     BInfo b2;
     if (AH == 3) {
         pos_adv(p3, kb, nr);
-        b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, S.cinfo[p3.ri * 64 + lane]);
+        b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, cinfo_at(L, S, p3.ri, lane, lanecol));
         bload8(ur, b2.seg, q);
         zq = bload1(ur, b2.zh, R());
     }
@@ -704,7 +734,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         pos_adv(pn, kb, nr);
         const bool nl = pn.vb >= 0 && (pn.zbs & 1) == 1;
         const uint32_t sn = nl ? brick_info<R, RZ, ZSH>(L, kb, S, pn, nstream, lx, ly, bc,
-                                                         S.cinfo[pn.ri * 64 + lane]).seg
+                                                         cinfo_at(L, S, pn.ri, lane, lanecol)).seg
                                : OOB;
         const bool nlp = dpp_swap_pair((unsigned)nl) != 0u;
         const uint32_t snp = dpp_swap_pair(sn);
@@ -793,7 +823,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         // latency per step instead of two)
         pos_adv(p3, kb, nr);
         pos_adv(pe, kb, nr);
-        const u2v ci3 = S.cinfo[p3.ri * 64 + lane], cie = S.cinfo[pe.ri * 64 + he];
+        const u2v ci3 = cinfo_at(L, S, p3.ri, lane, lanecol), cie = cinfo_at(L, S, pe.ri, he, hcol);
         __builtin_amdgcn_sched_barrier(0);     // keep the two reads ahead of every use
         const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, ci3);
         if (AH == 3) {
@@ -911,7 +941,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             TRAF(S, 3, changed, 8 * sizeof(R));
         }
         if (!LAZYN) u0_store();
-        if (changed) S.lastchg[b0.bid] = clock0 + b0.clk;   // lanes of one block write the same value
+        if (changed) S.lastchg[b0.bid] = (typename Smem<R, CMP>::clk_t)(clock0 + b0.clk);   // lanes of one block write the same value
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < 8; i++) {
@@ -964,11 +994,47 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     return nstream;
 }
 
+// Start of an iteration (compact layout): every block's pending state (it
+// changed at its last visit, or a face neighbour changed since) becomes
+// lastchg 1 / 0 against lastproc 1 and the clock restarts at 64
+// (fsm16_kernel.hip iter_norm; nothing is in flight across an iteration
+// boundary, so the decisions are those of unbounded clocks).
+template <typename R>
+__device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem<R, true> &S)
+{
+    const int nt = L.ntiles, nzk = L.nzk;
+    unsigned pend = 0;                       // bit i: block lane + 64 i (nblocks <= 1024)
+    for (int i = 0; i * 64 < L.nblocks; i++) {
+        const int b = threadIdx.x + 64 * i;
+        if (b >= L.nblocks) break;
+        const int tz = b / nt, id = b - tz * nt, ty = id / L.ntx, tx = id - ty * L.ntx;
+        const int lp = S.lastproc[b];
+        bool d = S.lastchg[b] >= lp;
+        if (tx > 0) d |= S.lastchg[b - 1] > lp;
+        if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
+        if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
+        if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
+        if (tz > 0) d |= S.lastchg[b - nt] > lp;
+        if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
+        if (d) pend |= 1u << i;
+    }
+    asm volatile("" ::: "memory");
+    for (int i = 0; i * 64 < L.nblocks; i++) {
+        const int b = threadIdx.x + 64 * i;
+        if (b >= L.nblocks) break;
+        S.lastproc[b] = 1;
+        S.lastchg[b] = (unsigned short)((pend >> i) & 1u);
+    }
+    asm volatile("" ::: "memory");
+}
+template <typename R>
+__device__ __forceinline__ void iter_norm(const FsmLaunch &, const Smem<R, false> &) {}
+
 // End-of-iteration check of the nodes below T (run only when no node >= T
 // changed): the z-blocks that changed in this iteration (lastchg >= the
 // iteration's first clock); u0 was stored at their first visit.
-template <typename R>
-__device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R> &S, int clock_it, bool &notconv)
+template <typename R, bool CMP>
+__device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u0r, const Smem<R, CMP> &S, int clock_it, bool &notconv)
 {
     const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
     const R T = (R)L.conv_thresh, tolr = (R)L.tol;
@@ -1012,7 +1078,8 @@ template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Smem<R> S = smem_bind<R, KB == MCEIK_KB && sizeof(R) == 4 && SLOWMODE == 2>(L, smem);
+    constexpr bool CMP = sizeof(R) == 8 && KB > 0;     // fsm_compact_layout() (the host checked it)
+    const Smem<R, CMP> S = smem_bind<R, KB == MCEIK_KB && sizeof(R) == 4 && SLOWMODE == 2, CMP>(L, smem);
     const int lane = threadIdx.x;
     const uint32_t fbytes = (uint32_t)(L.field_elems * sizeof(R));
     build_order(L, S.order);
@@ -1050,8 +1117,11 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         // are all u_nan updates to u_nan (a1 == u_nan), so it needs no visit
         // until a neighbour changes.  The stream clock starts at 64, so no
         // initial visit counts as in flight.
+        // (compact layout: 16-bit clocks relative to the iteration, the same
+        // order -- visited 2, changed 1, BC blocks changed 3 -- rebased by
+        // iter_norm at every iteration start, where the clock restarts at 64)
         for (int t = lane; t < L.nblocks; t += 64) {
-            S.lastproc[t] = -2; S.lastchg[t] = -3;
+            S.lastproc[t] = CMP ? 2 : -2; S.lastchg[t] = CMP ? 1 : -3;
         }
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
 #ifdef MCEIK_TRAFFIC
@@ -1068,7 +1138,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                 for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
                     for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
                         for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
-                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = -1;
+                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = CMP ? 3 : -1;
             }
         }
         asm volatile("" ::: "memory");
@@ -1077,6 +1147,10 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
+                if (CMP) {
+                    iter_norm(L, S);
+                    clock = 64;
+                }
                 const int clock_it = clock;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
@@ -1216,7 +1290,8 @@ static int variant(const FsmLaunch &L, int is_double)
 {
     const int mode = L.slow_mode == 0 ? 0 : (L.cell_cache ? 2 : 1);
     if (is_double) {
-        const int v = 9 + mode * 2 + (mode == 2 && L.nrz == 4 && L.ccb <= 64 ? (L.kb == MCEIK_KB ? 2 : 1) : 0);
+        // compile-time kb (15, 16) iff the compact LDS layout applies (nblocks <= MCEIK_MAX_BLOCKS)
+        const int v = 9 + mode * 2 + (mode == 2 && L.nrz == 4 && L.ccb <= 64 ? (fsm_compact_layout(L, 8) ? 2 : 1) : 0);
         return v == 15 && L.fast_sqrt ? 16 : v;      // the fp64 sampler instance with the short sqrt
     }
     if (mode != 2) return mode * 2;

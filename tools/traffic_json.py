@@ -5,7 +5,8 @@ WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction, KB x 1024), the SQ
 instruction counters and the VALU per wave macro step -- the fp32 record at
 the top level (bench.py's headline) and the fp64 record under "f64" (the
 line's f64 record).
-usage: tools/traffic_json.py <dir> <kernel_rev> [round] [f64_dir] > profiles/traffic.json"""
+usage: tools/traffic_json.py <dir> <kernel_rev> [round] [f64_dir] [f64_kernel_rev] > profiles/traffic.json
+(the fp32 record from <dir>; the fp64 record from f64_dir, default <dir>)"""
 import csv
 import collections
 import glob
@@ -74,9 +75,10 @@ def main():
     d, rev = sys.argv[1], sys.argv[2]
     rnd = int(sys.argv[3]) if len(sys.argv) > 3 else 4
     d64 = sys.argv[4] if len(sys.argv) > 4 else d
+    rev64 = sys.argv[5] if len(sys.argv) > 5 else rev
     out = record(d, 32, rev, rnd)
     if os.path.isdir(os.path.join(d64, "f64_pmc1")):
-        out["f64"] = record(d64, 64, rev, rnd)
+        out["f64"] = record(d64, 64, rev64, rnd)
     json.dump(out, sys.stdout, indent=1)
     print()
 
