@@ -193,6 +193,11 @@ int mceik_fsm_batch_solve(const mceik_fsm_batch *b, void *workspace, size_t work
 /* z nodes per macro step the launch of this batch runs (8 or 16; diagnostic). */
 int mceik_fsm_step_z(const mceik_fsm_batch *b);
 
+/* The kernel instance the launch of this batch runs (the name rocprofv3
+ * traces show) and its LDS bytes per wave; host-side, no GPU needed. */
+const char *mceik_fsm_kernel_name(const mceik_fsm_batch *b);
+size_t mceik_fsm_lds_bytes(const mceik_fsm_batch *b);
+
 /* Algorithmic HBM bytes of one node visit in one sweep (roofline accounting). */
 double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b);
 

@@ -93,6 +93,7 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_b
            "locate_l2_gridSearch__double64",
            "locate_l2_gridSearch__float64", "mceik_relocate",
            "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_fsm_step_z",
+           "mceik_fsm_kernel_name", "mceik_fsm_lds_bytes",
            "mceik_memcpy",
            "mceik_mcmc_init", "mceik_mcmc_run", "mceik_mcmc_set_stream", "mceik_mcmc_sync",
            "mceik_mcmc_get_state", "mceik_mcmc_get_samples", "mceik_mcmc_last", "mceik_mcmc_fsm_stats",
@@ -135,6 +136,10 @@ def lib():
     L.mceik_fsm_workspace_bytes.argtypes = [C.POINTER(FsmBatch)]
     L.mceik_fsm_step_z.restype = C.c_int
     L.mceik_fsm_step_z.argtypes = [C.POINTER(FsmBatch)]
+    L.mceik_fsm_kernel_name.restype = C.c_char_p
+    L.mceik_fsm_kernel_name.argtypes = [C.POINTER(FsmBatch)]
+    L.mceik_fsm_lds_bytes.restype = C.c_size_t
+    L.mceik_fsm_lds_bytes.argtypes = [C.POINTER(FsmBatch)]
     L.mceik_fsm_bytes_per_node_sweep.restype = C.c_double
     L.mceik_fsm_bytes_per_node_sweep.argtypes = [C.POINTER(FsmBatch)]
     L.mceik_fsm_batch_solve.restype = C.c_int

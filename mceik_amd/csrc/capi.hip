@@ -245,6 +245,22 @@ extern "C" int mceik_fsm_step_z(const mceik_fsm_batch *b)
     return fsm_launch_kind(L, b->precision == 64);
 }
 
+extern "C" const char *mceik_fsm_kernel_name(const mceik_fsm_batch *b)
+{
+    if (!b) return "";
+    FsmLaunch L;
+    fill_launch(L, b);
+    return fsm_launch_name(L, b->precision == 64);
+}
+
+extern "C" size_t mceik_fsm_lds_bytes(const mceik_fsm_batch *b)
+{
+    if (!b) return 0;
+    FsmLaunch L;
+    fill_launch(L, b);
+    return fsm_launch_lds_bytes(L, b->precision == 64);
+}
+
 extern "C" double mceik_fsm_bytes_per_node_sweep(const mceik_fsm_batch *b)
 {
     // u read + u write per node visit; slowness read once per node per model

@@ -19,7 +19,7 @@ def _declared_functions():
     for h in ("mceik.h", "mceik_eikonal.h", "os.h"):
         txt = open(os.path.join(INC, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-        for m in re.finditer(r"^\s*(?:int|void|size_t|double|bool)\s+\**\s*([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
+        for m in re.finditer(r"^\s*(?:int|void|size_t|double|bool|const char)\s+\**\s*([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
             names.add(m.group(1))
     return names
 

@@ -6,6 +6,7 @@
   to the fp64 oracle.
 On a mismatch the test bisects the sweep budget to name the first bad sweep.
 """
+import ctypes as C
 import glob
 import os
 
@@ -171,17 +172,31 @@ def test_fp64_batch_bitwise_vs_oracle(case):
     assert int(out["ierr"][0]) == ierr
 
 
-@pytest.mark.parametrize("nz,max_waves,fast", [(34, 0, False), (34, 0, True), (67, 2, True)],
-                         ids=["kb4", "kb4_short_sqrt", "kb4_short_sqrt_ragged_reuse"])
-def test_fp64_inversion_grid_mode_bitwise(nz, max_waves, fast):
+F64_GRID = {"kb4": "fsm_solve_kernel<double, 2, false, 2, 1, 4>",
+            "kb4_short_sqrt": "fsm_solve_kernel<double, 2, true, 2, 1, 4>",
+            "kb4_short_sqrt_ragged_reuse": "fsm_solve_kernel<double, 2, true, 2, 1, 4>",
+            "kb3_runtime_kb": "fsm_solve_kernel<double, 2, false, 2, 1, 0>",
+            "over_1024_blocks": "fsm_solve_kernel<double, 2, false, 2, 1, 0>"}
+
+
+@pytest.mark.parametrize("nz,max_waves,fast,nxy,case",
+                         [(34, 0, False, None, "kb4"), (34, 0, True, None, "kb4_short_sqrt"),
+                          (67, 2, True, None, "kb4_short_sqrt_ragged_reuse"), (20, 0, True, None, "kb3_runtime_kb"),
+                          (32, 0, True, 264, "over_1024_blocks")],
+                         ids=list(F64_GRID))
+def test_fp64_inversion_grid_mode_bitwise(nz, max_waves, fast, nxy, case):
     """The fp64 sampler's kernel (bench.py --precision 64): per-cell fp32
     slowness, fp64 fields and the literal update.  Several models and stations
     per launch (max_waves 2: several solves per wave in reused scratch);
     fields, event tables, iterations bitwise = the fp64 oracle on the expanded
     field.  fast=True is the instance the sampler launches (the short sqrt,
-    bare v_min/v_max_f64: fsm_update.h godunov_fast64)."""
+    bare v_min/v_max_f64: fsm_update.h godunov_fast64) with the compact LDS
+    layout (16-bit block clocks rebased per iteration, whole-line own loads);
+    kb != 4 and more than 1024 z-blocks fall back to the runtime-kb instance."""
     dev = _dev()
     nx, ny, h, nref = 30, 26, 100.0, (4, 4, 4)
+    if nxy:
+        nx = ny = nxy
     ncx, ncy, ncz = [-(-a // r) for a, r in zip((nx, ny, nz), nref)]
     rng = np.random.default_rng(23)
     nmodel = 2
@@ -190,9 +205,14 @@ def test_fp64_inversion_grid_mode_bitwise(nz, max_waves, fast):
     k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
     src = np.array([[[0.0, 1234.5, 987.6, (nz - 1) * h]], [[0.0, 300.0, 2200.0, (nz - 1) * h]],
                     [[0.1, 1500.0, 1200.0, 1700.0]]])
+    if nxy:
+        nmodel, v, scell, src = 1, v[:1], scell[:1], src[:1]
     ev = rng.integers(0, nx * ny * nz, 7).astype(np.int32)
     from mceik_amd.eikonal import BatchSolver
+    from mceik_amd import _lib
     bs = BatchSolver(nx, ny, nz, h, 0.0, 0.0, 0.0, 50, 1e-8, 64, nref=nref, fast_sqrt=fast)
+    kname = _lib.lib().mceik_fsm_kernel_name(C.byref(bs.describe(nmodel, len(src), 1, 1, nev=len(ev)))).decode()
+    assert kname == F64_GRID[case], kname
     out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(nmodel, -1), device=dev),
                    ev_node=torch.tensor(ev), want_fields=True, max_waves=max_waves)
     assert out["step_z"] == 8
