@@ -1180,9 +1180,6 @@ __device__ __forceinline__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, 
                     if (x < L.nx && y < L.ny && zb * 8 + i < L.nz && u[i] < T && !(dl < tolr)) notconv = true;
                 }
             }
-            // the iteration is not converged once any node fails: the rest of
-            // the scan cannot change the answer (its only output), so stop
-            if (__any(notconv)) return;
         }
     }
 }

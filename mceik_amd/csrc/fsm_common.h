@@ -115,6 +115,9 @@ static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b
 #define MCEIK_F64_FL 1           // fp64 compile-time-kb instances: whole-line own loads
 #endif
 #define MCEIK_F64_HOLD (2 * 64 * 16)
+#ifndef MCEIK_VERIFY_EARLY_EXIT
+#define MCEIK_VERIFY_EARLY_EXIT 1  // convergence verify stops at the first failing node (0: full scan, A/B)
+#endif
 #define MCEIK_SMEM_ARRAYS 12
 #define MCEIK_XROWS 80           // neighbour-row array: 64 lanes + 8 x-halo + 8 y-halo rows
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }

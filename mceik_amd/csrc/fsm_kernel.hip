@@ -1064,7 +1064,7 @@ __device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u
             }
             // the iteration is not converged once any node fails: the rest of
             // the scan cannot change the answer (its only output), so stop
-            if (__any(notconv)) return;
+            if (MCEIK_VERIFY_EARLY_EXIT && __any(notconv)) return;
         }
     }
 }
