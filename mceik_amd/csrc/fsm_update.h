@@ -235,6 +235,9 @@ __device__ __forceinline__ double sqrt_normal_f64(double x)
     return __builtin_fma(d, h, g);
 }
 
+#ifndef MCEIK_F64_NOCLAMP
+#define MCEIK_F64_NOCLAMP 0      // 1: drop the 3D root clamp (measured 1.1% slower, profiles/r04_ncl)
+#endif
 #ifndef MCEIK_F64_NOBRANCH
 #define MCEIK_F64_NOBRANCH 0     // 1: the fast fp64 update as straight-line code (A/B)
 #endif
@@ -270,6 +273,15 @@ __device__ __forceinline__ double godunov_fast64(double a, double b, double c, d
     const unsigned long long b3 = __builtin_bit_cast(unsigned long long, dmin_(x3, UN));
     const unsigned long long b23 = (__builtin_bit_cast(unsigned long long, x2) & m2) | (b3 & ~m2);
     return __builtin_bit_cast(double, (__builtin_bit_cast(unsigned long long, x1) & m1) | (b23 & ~m1));
+#elif MCEIK_F64_NOCLAMP
+    // The reference clamps the 3D root at u_nan.  The 3D case is selected
+    // only when x1 > a2 and x2 > a3: with a2 = u_nan x1 = a1 + f cannot exceed
+    // it (a1 + f rounds to u_nan at most), with a3 = u_nan the 2D root cannot
+    // (it is a1-based, finite or x1), so a1..a3 are travel times, all finite
+    // and far below u_nan / 4, and x3 = (-qb + sqrt(disc)) / 2 is too: the
+    // clamp never acts on a selected value.  Dropping it drops the u_nan
+    // constant (an SGPR pair the kernel spills) from the node update.
+    return r1 ? x1 : r2 ? x2 : x3;
 #else
     return r1 ? x1 : r2 ? x2 : (x3 < UN ? x3 : UN);
 #endif
