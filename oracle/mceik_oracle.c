@@ -299,6 +299,9 @@ typedef struct {
     const unsigned char *skip;    /* NULL or [nphase][nstat]: no table for (phase, station) -- the station
                                      has no picks of that phase (lhasP / lhasS, homog.c:313-335); its
                                      table row is FLT_MAX (the sampler's rule, mceik_fsm_batch.skip) */
+    int prec;                     /* 64: the fp64 sampler (--precision 64): per-cell fp32 slowness 1/(float)v
+                                     promoted to fp64, the literal fp64 solve (bitwise the reference on the
+                                     goldens), tables (float)u; otherwise the fp32 twin */
 } oracle_mcmc_problem;
 
 /* Travel time of an event from a solved fp32 field u (x fastest).  w == NULL:
@@ -367,9 +370,19 @@ static int oracle_forward_phase_f32(const oracle_mcmc_problem *p, int ph, const 
         float *u = (float *)malloc(n * sizeof(float));
         double ts = 0.0;
         int it = 0;
-        nerr += oracle_eikonal3d_solve_f32(p->maxit, 1, p->nx, p->ny, p->nz, p->tol, p->h,
-                                           p->x0, p->y0, p->z0, &ts, &p->sx[s], &p->sy[s],
-                                           &p->sz[s], slow, u, &it) != 0;
+        if (p->prec == 64) {
+            double *s64 = (double *)malloc(n * sizeof(double)), *u64 = (double *)malloc(n * sizeof(double));
+            for (size_t i = 0; i < n; i++) s64[i] = (double)slow[i];
+            nerr += oracle_eikonal3d_solve_f64(p->maxit, 1, p->nx, p->ny, p->nz, p->tol, p->h,
+                                               p->x0, p->y0, p->z0, &ts, &p->sx[s], &p->sy[s],
+                                               &p->sz[s], s64, u64, &it) != 0;
+            for (size_t i = 0; i < n; i++) u[i] = (float)u64[i];    /* the GPU's table export, fsm_device.h event_time */
+            free(s64); free(u64);
+        } else {
+            nerr += oracle_eikonal3d_solve_f32(p->maxit, 1, p->nx, p->ny, p->nz, p->tol, p->h,
+                                               p->x0, p->y0, p->z0, &ts, &p->sx[s], &p->sy[s],
+                                               &p->sz[s], slow, u, &it) != 0;
+        }
         if (niter) niter[s] = it;
         for (int e = 0; e < p->nevents; e++)
             ttab[(size_t)s * p->nevents + e] = oracle_event_time(u, p->nx, p->ny, p->nz, p->ev_node[e],

@@ -129,12 +129,14 @@ class McmcProblem(C.Structure):
                                           "tobs", "tcorr", "var")] + \
                [("vmin", C.c_int), ("vmax", C.c_int), ("dvmax", C.c_int), ("seed", C.c_uint32),
                 ("ev_frac", C.c_void_p), ("nphase", C.c_int), ("vsmin", C.c_int), ("vsmax", C.c_int),
-                ("obs_phase", C.c_void_p), ("skip", C.c_void_p)]
+                ("obs_phase", C.c_void_p), ("skip", C.c_void_p), ("prec", C.c_int)]
 
 
-def make_problem(pb):
-    """pb: mceik_amd.mcmc.Problem-like object holding numpy arrays. Keeps refs alive."""
+def make_problem(pb, precision=32):
+    """pb: mceik_amd.mcmc.Problem-like object holding numpy arrays. Keeps refs alive.
+    precision 64: the fp64 sampler's forward (oracle_mcmc_problem.prec)."""
     P = McmcProblem()
+    P.prec = int(precision)
     for n in ("nx", "ny", "nz", "nrx", "nry", "nrz", "ncx", "ncy", "ncz", "maxit", "nstat", "nevents",
               "vmin", "vmax", "dvmax"):
         setattr(P, n, int(getattr(pb, n)))

@@ -135,6 +135,41 @@ def test_c3_fp64_sampler_tables_bitwise():
 
 
 @pytest.mark.timeout(600)
+def test_c2_fp64_sampler_mcmc_bitwise():
+    """The fp64 sampler's MCMC path (bench.py's f64 record: the short-sqrt
+    fp64 instance, compact LDS, whole-line loads): C2 geometry, chains 3 and
+    4 -- init tables, iterations and logL, then models, logL and accept
+    counts after three steps == oracle_mcmc_run with the fp64 forward
+    (oracle_mcmc_problem.prec = 64: the literal fp64 solve on the per-cell
+    fp32 slowness, tables (float)u)."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _problem("C2")
+    p.dvmax = 400
+    p.var[:] = 1e-6
+    nsteps = 3
+    s = mcmc.Sampler(p, nchains=2, chain_offset=3, precision=64)
+    assert s.info()["kernel"] == "fsm_solve_kernel<double, 2, true, 2, 1, 4>", s.info()["kernel"]
+    v0, logl0, _, _ = s.state()
+    ttab, niter, _, ierr = s.last(with_ierr=True)
+    assert not ierr.any()
+    s.run(nsteps)
+    v1, logl1, nacc1, step = s.state()
+    s.close()
+    assert step == nsteps
+    P = O.make_problem(p, precision=64)
+    for c in range(2):
+        tt, it = O.forward_f32(P, v0[c])
+        assert np.array_equal(ttab[c].view(np.uint32), tt.view(np.uint32)), c
+        assert np.array_equal(niter[c], it), c
+        assert logl0[c] == O.loglik(P, tt), c
+    vo, lo, acc, _ = O.mcmc_run(P, v0, logl0, 3, 0, nsteps)
+    assert np.array_equal(v1, vo)
+    assert np.array_equal(logl1.view(np.uint64), lo.view(np.uint64))
+    assert np.array_equal(nacc1, acc.sum(0))
+
+
+@pytest.mark.timeout(600)
 def test_c5_sampler_launch_bitwise():
     """C5 through the sampler: 256^3, 64 stations, 32 chains = 2048 solves per
     step on scratch-budget-capped waves (the runtime-kb fsm16 instance with
