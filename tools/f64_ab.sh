@@ -1,6 +1,7 @@
-# fp64 sampler instance A/B on one box: each variant's libmceik_hip.so (mceik_amd/exp/lib_<v>.so;
-# v:N caps the resident waves at N) runs the C3 one-pipe bench (precisions AB_PRECS, default 64) twice, interleaved;
-# then the fp64 parity tests on each variant in F64_TEST
+# Sampler-kernel A/B on one box: each variant's libmceik_hip.so (mceik_amd/exp/lib_<v>.so;
+# v:N caps the resident waves at N) runs the C3 one-pipe bench for each precision in
+# AB_PRECS (default 64) with AB_STEPS timed steps (default 1), two interleaved rounds;
+# then the fp64 parity tests on each variant in F64_TEST.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${F64_OUT:-f64e}
@@ -10,13 +11,12 @@ for r in 1 2; do for vv in ${F64_VARIANTS:-f64a f64b f64c}; do
   v=${vv%%:*}; mw=0; [ "$v" != "$vv" ] && mw=${vv#*:}
   cp mceik_amd/exp/lib_$v.so mceik_amd/libmceik_hip.so
   for prec in ${AB_PRECS:-64}; do
-  timeout -k 10 300 python3 bench.py --precision $prec --steps ${AB_STEPS:-1} --warmup 1 --no-cpu-baseline --pipes 1 \
-      --max-waves $mw --f64-steps 0 > $O/${v}_mw${mw}_p${prec}_$r.log 2>&1
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" $O/${v}_mw${mw}_p${prec}_$r.log ${v}_mw${mw}_p$prec | tee -a $O/summary.txt
+    log=$O/${v}_mw${mw}_p${prec}_$r.log
+    timeout -k 10 300 python3 bench.py --precision $prec --steps ${AB_STEPS:-1} --warmup 1 --no-cpu-baseline --pipes 1 \
+        --max-waves $mw --f64-steps 0 > $log 2>&1
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" \
+        $log ${v}_mw${mw}_p$prec | tee -a $O/summary.txt
   done
-  continue
-  v=${v}_mw$mw
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])" $O/${v}_$r.log $v | tee -a $O/summary.txt
 done; done
 for t in ${F64_TEST:-}; do
   cp mceik_amd/exp/lib_$t.so mceik_amd/libmceik_hip.so
