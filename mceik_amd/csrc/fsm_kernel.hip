@@ -525,6 +525,11 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
 {
     const int lane = threadIdx.x;
     const R T = (R)L.conv_thresh;
+    // MCEIK_BIGSTEP (fp64): a node that drops by >= tol (1 + 2^-50) in one
+    // update moved by >= tol over the iteration (values only fall), so the
+    // reference's |u0 - u| < tol fails: not converged, as the >= T rule says
+    // in fp32 (where T = 2^26 s makes that rule empty in fp64)
+    const R TB = (R)(L.tol * (1.0 + 0x1p-50));
     const int fl = b0.fl;
     bool xp = true, xn = true, yp = true, yn = true, act = true;
     if (GENERIC) {
@@ -607,7 +612,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
             nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv, ffv, CELLF ? ff2c : ffv + ffv, CELLF ? ff3c : (R)3 * ffv));
         }
         const bool dec = nv < self;
-        nc |= dec && self >= T;
+        nc |= dec && (self >= T || (MCEIK_BIGSTEP && sizeof(R) == 8 && self - nv >= TB));
         changed |= dec;
         r[pj] = nv;
     }
@@ -893,8 +898,10 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             }
         }
         // u0: a block's first visit in the iteration (old values c)
+        // (MCEIK_BIGSTEP: once the iteration is known unconverged its
+        // verify never runs, so its remaining u0 copies are not needed)
         auto u0_store = [&]() __attribute__((always_inline)) {
-            if (!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) {
+            if ((!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) && !(MCEIK_BIGSTEP && __any(notconv))) {
                 R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
                 const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
                 if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
