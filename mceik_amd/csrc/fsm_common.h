@@ -116,7 +116,7 @@ static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b
 #endif
 #define MCEIK_F64_HOLD (2 * 64 * 16)
 #ifndef MCEIK_BIGSTEP
-#define MCEIK_BIGSTEP 0            // 1: fp64 early non-convergence from single big updates, u0 copies skipped after (v34 candidate)
+#define MCEIK_BIGSTEP 1            // fp64 early non-convergence from single big updates, u0 copies skipped after (v34; 0: A/B)
 #endif
 #ifndef MCEIK_VERIFY_EARLY_EXIT
 #define MCEIK_VERIFY_EARLY_EXIT 1  // convergence verify stops at the first failing node (0: full scan, A/B)
