@@ -12,6 +12,12 @@ chains) and gathers the kept posterior states to rank 0 over RCCL at the
 end of the timed region (the checkpoint).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+ranks itself (torch.distributed.run on 127.0.0.1, one process per GPU, before
+anything touches the GPU) and exits with their status; under an external
+launcher WORLD_SIZE must equal --gpus.  An N > 1 run exits non-zero when the
+gathered posterior differs from the ranks' own shards.
 """
 import argparse
 import ctypes as C
@@ -123,8 +129,87 @@ def cpu_baseline(p, v0, cores, rounds=CPU_ROUNDS):
                       f"{float(np.max(times)):.3f} s; proposals/s = cores / median / {p.nstat} stations"}
 
 
+def node_gpus():
+    """GPU agents of this host from the KFD topology (every GPU of the node,
+    whether or not this process may use it; sysfs only, no GPU call), or None."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for d in os.listdir(base):
+            with open(os.path.join(base, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+    except (OSError, ValueError):
+        return None
+    return n or None
+
+
+def core_share(cpu):
+    """The baseline against one GPU's share of the node's cores (host CPUs /
+    GPUs on the node), next to the allotted `cores` the leg actually used;
+    the share's rate assumes the reference's table-parallel solves scale
+    linearly with cores (they are independent single-threaded solves)."""
+    host, ngpu = os.cpu_count() or 1, node_gpus()
+    cpu["host_cpus"] = host
+    cpu["gpus_on_node"] = ngpu
+    if ngpu:
+        share = host // ngpu
+        cpu["per_gpu_share_cores"] = share
+        cpu["per_gpu_share_value"] = round(cpu["value"] * share / cpu["cores"], 5)
+    else:
+        cpu["per_gpu_share_cores"] = None        # no KFD topology (no GPU driver on this host)
+        cpu["per_gpu_share_value"] = None
+    return cpu
+
+
+# ---------------------------------------------------------------- ranks
+def launch_ranks(n):
+    """Start the N ranks of `--gpus N` (one process per GPU) under
+    torch.distributed.run on 127.0.0.1 with this command line, and return
+    their exit status.  Runs before this process touches the GPU; the ranks
+    find WORLD_SIZE set and run main() themselves."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def rank_fields(world, steps, per_rank, gather_path=None, gather_check=None, digest_check=None):
+    """The line's per-rank attribution: `rank_step_ms` {min, max, ranks} (each
+    rank's own time per step up to its synchronise), `gather_ms` (the slowest
+    rank's checkpoint gather) and, for N > 1, `ranks` and `gather` {path, ms,
+    equals_torch_gather, shards_match_ranks}.  per_rank: [[steps s, gather s]]
+    of every rank."""
+    st = [r[0] / steps * 1e3 for r in per_rank]
+    out = {"rank_step_ms": {"min": round(min(st), 2), "max": round(max(st), 2), "ranks": len(st)},
+           "gather_ms": round(max(r[1] for r in per_rank) * 1e3, 3)}
+    if world > 1:
+        out["ranks"] = world
+        # equals_torch_gather: the library's RCCL gather against torch.distributed's
+        # (None: no library communicator on this run, torch's gather was the timed path);
+        # shards_match_ranks: each rank's block of the gathered posterior = its own kept states
+        out["gather"] = {"path": gather_path, "ms": out["gather_ms"], "equals_torch_gather": gather_check,
+                         "shards_match_ranks": digest_check}
+    return out
+
+
+def shard_digest(v, logl):
+    """sha256 of a block of kept states (int32 models, fp64 logL), as bytes."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(v, dtype=np.int32).tobytes())
+    h.update(np.ascontiguousarray(logl, dtype=np.float64).tobytes())
+    return h.hexdigest()
+
+
 # ---------------------------------------------------------------- roofline
-def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config):
+def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config, kname=None):
     """The `roofline` object of a timed region: algorithmic bytes of the FSM
     launches (visited bricks x nodes x bytes per node sweep)
     over the FSM time of a step -- the HIP-event launch duration with one
@@ -139,11 +224,8 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config):
     b.nx, b.ny, b.nz, b.h = p.nx, p.ny, p.nz, p.h
     b.nmodel, b.nsrc, b.fast_sqrt, b.maxit, b.tol = per_gpu, 1, 1, p.maxit, p.tol
     b.nev = p.nevents
-    step_z = _lib.lib().mceik_fsm_step_z(C.byref(b))
-    kname = ("fsm16_solve_kernel (16-z steps, cells via LDS cache, fast sqrt, nrz=4)" if step_z == 16 else
-             "fsm_solve_kernel<float, 2, true, 2, 1, 4> (8-z steps, cells via LDS cache, fast sqrt, nrz=4)"
-             if precision == 32 else "fsm_solve_kernel<double, 2, true, 2, 1, 4> (8-z steps, fp64 literal update, "
-                                     "short sqrt, whole-line own loads, compact LDS: 8 waves/CU)")
+    if kname is None:
+        kname = _lib.lib().mceik_fsm_kernel_name(C.byref(b)).decode()
     # algorithmic bytes: every node of every VISITED 8x8x8 brick (z-blocks whose
     # inputs did not change since their last visit are skipped)
     nbricks = -(-p.nx // 8) * -(-p.ny // 8) * -(-p.nz // 8)
@@ -217,11 +299,13 @@ def f64_record(p, v0, per_gpu, args, dev, stream):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     stats = smp.fsm_stats()
+    info = smp.info()
     smp.close()
+    rl = roofline(p, per_gpu, 64, stats, elapsed, args.f64_steps, args.config, kname=info["kernel"])
+    rl["lds_bytes_per_wave"] = info["lds_bytes"]
     return {"value": round(per_gpu * args.f64_steps / elapsed, 3), "unit": "proposals/s", "dtype": "f64",
             "steps": args.f64_steps, "warmup": args.f64_warmup,
-            "ms_per_step": round(elapsed / args.f64_steps * 1e3, 2),
-            "roofline": roofline(p, per_gpu, 64, stats, elapsed, args.f64_steps, args.config)}
+            "ms_per_step": round(elapsed / args.f64_steps * 1e3, 2), "roofline": rl}
 
 
 
@@ -248,12 +332,29 @@ def main():
     ap.add_argument("--pipes", type=int, default=2, choices=(1, 2, 3, 4),
                     help="the sampler's chains as two halves on two streams (the library default, DESIGN.md "
                          "s.3.5) or one launch per step (1)")
+    ap.add_argument("--probe-ranks", action="store_true",
+                    help="each rank prints its rank and world size and exits before any GPU call "
+                         "(tests the --gpus launcher on a CPU host)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no external launcher: start the N ranks here, before any GPU call
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: the launcher's rank count must equal --gpus",
+              file=sys.stderr)
+        sys.exit(2)
     os.environ["MCEIK_PIPES"] = str(args.pipes)
 
     rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if args.probe_ranks:
+        print(json.dumps({"probe": "rank", "rank": rank, "world": world, "local_rank": local_rank,
+                          "gpus": args.gpus}), flush=True)
+        return 0
     # MCEIK_BENCH_REHEARSAL=1: rehearse the N > 1 flow on ONE GPU (every rank on
     # device 0, torch.distributed over gloo, host-side gather; RCCL takes one
     # rank per GPU, so the library communicator is skipped).  A correctness
@@ -274,7 +375,7 @@ def main():
     v0 = mcmc.initial_models(p, range(lo, hi))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(p, v0[0], args.cpu_cores or cpu_cores(), args.cpu_rounds)
+        cpu = core_share(cpu_baseline(p, v0[0], args.cpu_cores or cpu_cores(), args.cpu_rounds))
 
     import torch
     import torch.distributed as dist
@@ -287,14 +388,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
     red_dev = torch.device("cpu") if rehearse else dev      # where the small reductions live
     # picks from the GPU forward of the true model (replaces the analytic ones)
-    tt = mcmc.picks_from_forward(local_rank)(p)
+    # (+ pick noise sigma, varObs = sigma^2: the scale one proposal moves a travel time)
+    mcmc.bench_picks(p, args.sigma, local_rank)
     torch.cuda.empty_cache()             # the forward's workspace: the sampler sizes its waves to HBM
-    rng = np.random.default_rng(p.seed + 1)
-    # pick noise sigma and varObs = sigma^2 at the scale one proposal moves a
-    # travel time (~1 ms for 50 m/s on a 400-m cell), so the posterior is not
-    # flat at the proposal scale and Metropolis both accepts and rejects
-    p.tobs = tt.T.ravel().astype(np.float64) + rng.normal(0.0, args.sigma, p.nevents * p.nstat)
-    p.var[:] = args.sigma ** 2
     p.nburn, p.keepk = args.warmup, max(1, args.steps)
     smp = mcmc.Sampler(p, nchains=hi - lo, chain_offset=lo, v0=v0, max_samples=1, device=local_rank,
                        precision=args.precision, max_waves=args.max_waves)
@@ -366,15 +462,25 @@ def main():
         every = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
         per_rank = [e.tolist() for e in every]
-    gather_check = None
-    if world > 1 and comm is not None:
-        # outside the timed region: the library gather == torch.distributed's gather
-        tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=None if rehearse else dev)
-        if rank == 0:
-            gather_check = bool(torch.equal(tv.to(dev), post) and torch.equal(tl.to(dev), post_l))
+    gather_check = digest_check = None
+    if world > 1:
+        # outside the timed region, two checks of the gathered posterior:
+        # (1) with the library's RCCL gather, it equals torch.distributed's gather;
+        # (2) whatever the path, each rank's block of it equals the rank's own
+        #     kept states (sha256 of the shard, exchanged as objects)
         if comm is not None:
+            tv, tl = mcmc.gather_kept(smp, per_gpu * world, device=None if rehearse else dev)
+            if rank == 0:
+                gather_check = bool(torch.equal(tv.to(dev), post) and torch.equal(tl.to(dev), post_l))
             comm.close()
+        kv, kl = smp.samples(max_states=1)
+        digests = [None] * world
+        dist.all_gather_object(digests, (lo, hi, shard_digest(kv[0], kl[0])))
+        if rank == 0:
+            pv, pl = post.cpu().numpy(), post_l.cpu().numpy()
+            digest_check = all(shard_digest(pv[a:b], pl[a:b]) == d for a, b, d in digests)
     stats = smp.fsm_stats()
+    info = smp.info()
     _, logl, nacc, _ = smp.state()
     smp.close()
     f64 = None
@@ -383,7 +489,8 @@ def main():
 
     if rank == 0:
         total = per_gpu * world * args.steps
-        rl = roofline(p, per_gpu, args.precision, stats, elapsed, args.steps, args.config)
+        rl = roofline(p, per_gpu, args.precision, stats, elapsed, args.steps, args.config, kname=info["kernel"])
+        rl["lds_bytes_per_wave"] = info["lds_bytes"]
         line = {
             "metric": METRIC,
             "value": round(total / elapsed, 3),
@@ -408,16 +515,11 @@ def main():
             "accept_rate": round(float(nacc.sum()) / max(1, (hi - lo) * (args.warmup + args.steps)), 4),
         }
         if rehearse:
-            line["ranks"] = world
             line["rehearsal"] = "one GPU shared by all ranks (MCEIK_BENCH_REHEARSAL=1): not a scaling measurement"
-        st = [r[0] / args.steps * 1e3 for r in per_rank]
-        line["rank_step_ms"] = {"min": round(min(st), 2), "max": round(max(st), 2), "ranks": len(st)}
-        line["gather_ms"] = round(max(r[1] for r in per_rank) * 1e3, 3)
-        if world > 1:
-            line["gather"] = {"path": gather_path}
-            if gather_check is not None:
-                # the library's RCCL gather checked against torch.distributed's (outside the timed region)
-                line["gather"]["equals_torch_gather"] = gather_check
+        line.update(rank_fields(world, args.steps, per_rank, gather_path, gather_check, digest_check))
+        if cpu:
+            line["speedup_vs_cpu_per_gpu_share"] = (round(line["value"] / cpu["per_gpu_share_value"], 1)
+                                                    if cpu.get("per_gpu_share_value") else None)
         if args.raw_stats:
             ms, nl, it, (br, sg, sgc, ws) = stats
             line["fsm_raw"] = {"bricks": br, "segs": sg, "segs_changed": sgc, "iters": it, "wave_steps": ws,
@@ -427,9 +529,14 @@ def main():
         if cpu:
             line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
         print(json.dumps(line), flush=True)
+    bad = rank == 0 and (gather_check is False or digest_check is False)
     if world > 1:
         dist.destroy_process_group()
+    if bad:
+        print("bench: the gathered posterior differs from the ranks' own shards", file=sys.stderr)
+        return 3
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -135,8 +135,11 @@ typedef struct mceik_fsm_batch {
     int *niter, *ierr;          /* device [nmodel*nstat] or NULL             */
     int max_sweeps;             /* < 0: unlimited (debug)                    */
     unsigned long long *iter_total;  /* device counter += iterations of every solve, or NULL */
-    int fast_sqrt;              /* 1: caller guarantees h*slowness >= 1e-12 (cells mode, fp32):
-                                   use the shorter correctly rounded sqrt (same results) */
+    int fast_sqrt;              /* 1: caller guarantees h*slowness >= 1e-12 (cells mode, fp32 AND
+                                   fp64): fp32 uses the shorter correctly rounded sqrt, fp64 the
+                                   sqrt expansion without input scaling (both exact only for normal
+                                   radicands, hence the contract; same results within it).  0: the
+                                   full-range sqrt */
     unsigned long long *visit_stats; /* device [4] += brick visits (8x8x8 nodes, one sweep; z-blocks
                                         whose inputs did not change are skipped), column segments
                                         (8 nodes) updated, segments that changed, macro steps of the
@@ -167,7 +170,8 @@ typedef struct mceik_fsm_batch {
                                    without a phase map m % nphase, i.e. models [chain][phase]) is skipped when skip[ph*nstat + s] != 0 -- a
                                    station with no picks of that phase (mceik_stations_struct lhasP /
                                    lhasS; homog.c:313-335 builds tables only for flagged stations): no
-                                   sweep, niter 0, ierr 0, its ttab row FLT_MAX (the unreached value) */
+                                   sweep, niter 0, ierr 0, its ttab row FLT_MAX (the unreached value).
+                                   Refused together with u_out (a skipped solve has no field) */
     unsigned long long *solve_count; /* device counter += solves executed (not skipped), or NULL */
 } mceik_fsm_batch;
 

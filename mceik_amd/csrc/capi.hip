@@ -316,6 +316,11 @@ static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_
         fprintf(stderr, "mceik_fsm_batch_solve: workspace too small (%zu < %zu)\n", workspace_bytes, w.total);
         return 1;
     }
+    if (b->skip && b->u_out) {
+        // a skipped solve never sweeps, so its u slot would hold stale workspace
+        fprintf(stderr, "mceik_fsm_batch_solve: skip and u_out cannot be combined (a skipped solve has no field)\n");
+        return 1;
+    }
     hipStream_t st = (hipStream_t)stream;
     int is_double = b->precision == 64;
     FsmLaunch L;
@@ -2162,7 +2167,9 @@ extern "C" int mceik_mcmc_run(mceik_mcmc *s, int nsteps)
 
 // After a stream synchronisation: a multi-step launch whose wave gave up
 // waiting for a chain's step (the broken-queue flag) failed, and the chains'
-// state is not to be trusted; every later synchronising call reports it.
+// state is not to be trusted; every later synchronising call (and the
+// gather, through mcmc_shard_view) reports it until mceik_mcmc_restore
+// reloads a state.
 static int mc_queue_check(mceik_mcmc *s, const char *who)
 {
     if (!s->persist) return 0;
@@ -2243,6 +2250,10 @@ extern "C" int mceik_mcmc_restore(mceik_mcmc *s, const int *v, const double *log
     s->step = step;
     s->nkept = nkept;
     s->nkept_base = nkept;
+    if (s->persist) {
+        // the restored state replaces whatever a broken multi-step launch left: clear its flag
+        HIPCHK(hipMemset(s->d_sync + MC_SYNC_WORDS(s->D.nchains) - 1, 0, sizeof(unsigned)));
+    }
     return 0;
 }
 
@@ -2282,6 +2293,10 @@ int mcmc_shard_view(mceik_mcmc *s, int which, McmcShard *out)
     const McmcDev &D = s->D;
     out->device = s->device; out->stream = s->stream;
     out->nchains = D.nchains; out->chain_offset = D.chain_offset; out->ncell = D.ncm;
+    {   // a broken multi-step launch left no valid state to gather (-1)
+        DeviceScope dg(s->device);
+        if (hipStreamSynchronize(s->stream) != hipSuccess || mc_queue_check(s, "mceik_mcmc_gather")) return -1;
+    }
     if (which == 0) {
         out->v = D.v; out->logl = D.logl;
         return 0;
@@ -2342,6 +2357,7 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
     if (!s) return 1;
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
+    if (mc_queue_check(s, "mceik_mcmc_fsm_stats")) return -1;
     while (s->ev_folded < s->nlaunch) {
         if (fold_launch(s, s->ev_folded)) return -1;
         s->ev_folded++;
@@ -2377,6 +2393,7 @@ extern "C" int mceik_mcmc_fsm_solves(mceik_mcmc *s, unsigned long long *solves)
     if (!s || !solves) return 1;
     DeviceScope dg(s->device);
     HIPCHK(hipStreamSynchronize(s->stream));
+    if (mc_queue_check(s, "mceik_mcmc_fsm_solves")) return -1;
     HIPCHK(hipMemcpy(solves, s->d_iters + 5, sizeof(*solves), hipMemcpyDeviceToHost));
     return 0;
 }

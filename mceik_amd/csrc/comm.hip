@@ -142,9 +142,10 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
     if (!s || !c || root < 0 || root >= c->nranks || nchains_total < 1) return 1;
     DevScope dg(c->device);
     McmcShard sh;
-    const int have = mcmc_shard_view(s, which, &sh) == 0;
-    int status = 0;
-    if (sh.device != c->device) {
+    const int view = mcmc_shard_view(s, which, &sh);
+    const int have = view == 0;
+    int status = view < 0 ? -1 : 0;          // -1: the sampler's stream failed or its work queue broke
+    if (!status && sh.device != c->device) {
         fprintf(stderr, "mceik_mcmc_gather: sampler on device %d, communicator on %d\n", sh.device, c->device);
         status = 1;
     }

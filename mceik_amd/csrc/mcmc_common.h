@@ -37,4 +37,6 @@ struct McmcShard {
     const int *v;                  // device [nchains][ncell] (ncell = the chain's model entries)
     const double *logl;            // device [nchains]
 };
+// Returns 0, 1 (which = 1 and no state kept yet) or -1 (the sampler's stream
+// failed or a multi-step launch broke its work queue: no valid state).
 int mcmc_shard_view(mceik_mcmc *s, int which, McmcShard *out);

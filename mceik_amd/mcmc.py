@@ -520,6 +520,19 @@ def picks_from_forward(device=0, precision=64):
     return f
 
 
+def bench_picks(p: Problem, sigma=5e-4, device=0):
+    """bench.py's observations on `p` (in place): the GPU forward of the true
+    model (`picks_from_forward`) plus N(0, sigma) noise drawn with seed
+    p.seed + 1, and varObs = sigma^2 -- sigma at the scale one proposal moves
+    a travel time (~1 ms for 50 m/s on a 400-m cell), so Metropolis both
+    accepts and rejects (DESIGN.md s.7 "Accept rate")."""
+    tt = picks_from_forward(device)(p)
+    rng = np.random.default_rng(p.seed + 1)
+    p.tobs = tt.T.ravel().astype(np.float64) + rng.normal(0.0, sigma, p.nevents * p.nstat)
+    p.var[:] = sigma ** 2
+    return p
+
+
 def gather_kept(smp: Sampler, nchains_total, group=None, dst=0, device=None):
     """Checkpoint gather (SURVEY s.8e): the most recent kept state of every
     chain on every rank -> rank `dst`, in global chain order.

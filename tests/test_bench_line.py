@@ -55,3 +55,73 @@ def test_roofline_accounting(precision):
     assert r["traffic"] == rec["hbm_bytes_per_launch"]
     assert r["kernel_rev"] == bench.KERNEL_REVS[precision]
     assert ("fsm16_solve_kernel" in r["kernel"]) == (precision == 32)
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` with no external launcher starts 2 ranks itself
+    (torch.distributed.run on 127.0.0.1); --probe-ranks stops each rank before
+    any GPU call and prints its rank and world size."""
+    r = _run_bench(["--gpus", "2", "--probe-ranks"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    probes = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"probe"')]
+    assert sorted(q["rank"] for q in probes) == [0, 1], r.stdout
+    assert all(q["world"] == 2 and q["gpus"] == 2 for q in probes)
+    r1 = _run_bench(["--probe-ranks"])
+    assert r1.returncode == 0 and [json.loads(l)["world"] for l in r1.stdout.splitlines()] == [1]
+
+
+def test_world_size_must_equal_gpus():
+    """Under an external launcher WORLD_SIZE must equal --gpus (the driver's
+    SCALE line would otherwise mislabel its rank count)."""
+    r = _run_bench(["--gpus", "4", "--probe-ranks"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+    r = _run_bench(["--probe-ranks"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+
+
+def test_rank_fields_of_an_n_gt_1_line():
+    """Every N > 1 line carries ranks, rank_step_ms {min, max, ranks},
+    gather_ms and gather {path, ms, equals_torch_gather, shards_match_ranks}."""
+    import bench
+    f = bench.rank_fields(2, 4, [[8.0, 0.002], [8.4, 0.003]], "mceik_mcmc_gather (RCCL)", True, True)
+    assert f["ranks"] == 2
+    assert f["rank_step_ms"] == {"min": 2000.0, "max": 2100.0, "ranks": 2}
+    assert f["gather_ms"] == 3.0
+    assert f["gather"] == {"path": "mceik_mcmc_gather (RCCL)", "ms": 3.0, "equals_torch_gather": True,
+                           "shards_match_ranks": True}
+    one = bench.rank_fields(1, 4, [[8.0, 0.001]])
+    assert "gather" not in one and one["rank_step_ms"]["ranks"] == 1
+
+
+def test_shard_digest_detects_a_changed_state():
+    import numpy as np
+    import bench
+    v = np.arange(12, dtype=np.int32).reshape(3, 4)
+    lg = np.array([-1.0, -2.0, -3.0])
+    d = bench.shard_digest(v, lg)
+    assert bench.shard_digest(v.copy(), lg.copy()) == d
+    v2 = v.copy(); v2[1, 2] += 1
+    assert bench.shard_digest(v2, lg) != d
+    assert bench.shard_digest(v, np.nextafter(lg, 0.0)) != d
+
+
+def test_cpu_core_share_fields():
+    """cpu_baseline carries the host's CPUs, the GPUs on the node and one GPU's
+    share of the cores (None without a KFD topology, as on this CPU host)."""
+    import bench
+    c = bench.core_share({"value": 0.32, "cores": 16})
+    assert c["host_cpus"] == (os.cpu_count() or 1)
+    if c["gpus_on_node"]:
+        share = c["host_cpus"] // c["gpus_on_node"]
+        assert c["per_gpu_share_cores"] == share
+        assert c["per_gpu_share_value"] == pytest.approx(0.32 * share / 16, rel=1e-4)
+    else:
+        assert c["per_gpu_share_cores"] is None and c["per_gpu_share_value"] is None

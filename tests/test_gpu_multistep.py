@@ -100,9 +100,26 @@ def test_multi_step_broken_queue_is_reported(monkeypatch):
     monkeypatch.setenv("MCEIK_MC_SPIN_LIMIT", "0")
     s = mcmc.Sampler(p, nchains=64, max_samples=8)
     assert s.info()["multi_step"]
+    ck = s.checkpoint()
     s.run(8)
     with pytest.raises(RuntimeError):
         s.sync()
     with pytest.raises(RuntimeError):
         s.state()
+    with pytest.raises(RuntimeError):
+        s.fsm_stats()
+    with pytest.raises(RuntimeError):
+        s.fsm_solves()
+    # the checkpoint gather refuses the broken state too (single-rank RCCL communicator)
+    comm = mcmc.Comm(0, 1, 0)
+    with pytest.raises(RuntimeError):
+        comm.gather(s, 64, which=0)
+    # restoring a checkpoint replaces the state and clears the flag
+    s.restore(ck)
+    v, logl, nacc, step = s.state()
+    assert step == ck["step"] and np.array_equal(v, ck["v"])
+    assert np.array_equal(logl.view(np.uint64), ck["logl"].view(np.uint64))
+    vg, lg = comm.gather(s, 64, which=0)
+    assert np.array_equal(vg, ck["v"])
+    comm.close()
     s.close()

@@ -208,17 +208,20 @@ def test_ps_posterior_writes_s_tables(tmp_path):
                     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (m, ph, st)
 
 
-@pytest.mark.parametrize("mode", ["pipes2", "multi"])
+@pytest.mark.parametrize("mode", ["pipes2", "multi", "f64_pipes2"])
 def test_station_flags_skip_solves_bitwise(mode, monkeypatch):
     """Half the stations have no S picks (lhasS = 0, homog.c:313-335 makes no
     table for them): their S solves are skipped (table FLT_MAX, niter 0), the
     P tables of every station and the S tables of the others are the twin's,
     logL, accept sequence and both models after 6 steps == oracle_mcmc_run
     (with the same skip rule), and mceik_mcmc_fsm_solves counts only the
-    solves that ran."""
+    solves that ran.  f64_pipes2: the fp64 sampler (fsm_solve_kernel<double>,
+    the skip path of fsm_kernel.hip) against the fp64 oracle forward
+    (oracle_mcmc_problem.prec = 64)."""
     _dev()
+    prec = 64 if mode.startswith("f64") else 32
     monkeypatch.setenv("MCEIK_PERSIST", "1" if mode == "multi" else "0")
-    monkeypatch.setenv("MCEIK_PIPES", "2" if mode == "pipes2" else "1")
+    monkeypatch.setenv("MCEIK_PIPES", "1" if mode == "multi" else "2")
     from mceik_amd import mcmc
     p = _ps_problem(nstat=6)
     nos = np.arange(p.nstat) % 2 == 1                     # stations 1, 3, 5: no S picks
@@ -226,13 +229,14 @@ def test_station_flags_skip_solves_bitwise(mode, monkeypatch):
     hp, hs = p.station_flags()
     assert hp.all() and np.array_equal(hs, (~nos).astype(np.int32))
     nch, off, nsteps = 4, 3, 6
-    s = mcmc.Sampler(p, nchains=nch, chain_offset=off)
+    s = mcmc.Sampler(p, nchains=nch, chain_offset=off, precision=prec)
     assert s.info()["multi_step"] == (mode == "multi")
+    assert s.info()["kernel"].startswith("fsm_solve_kernel<double" if prec == 64 else "fsm16_solve_kernel")
     v0, logl0, _, _ = s.state()
     tt, niter, _, ierr = s.last(with_ierr=True)
     assert not ierr.any()
     assert (tt[:, 1, nos] == np.float32(np.finfo(np.float32).max)).all() and (niter[:, 1, nos] == 0).all()
-    P = O.make_problem(p)
+    P = O.make_problem(p, precision=prec)
     for c in range(nch):
         to = O.forward_all_f32(P, v0[c])
         assert np.array_equal(tt[c].view(np.uint32), to.view(np.uint32)), c

@@ -1,22 +1,32 @@
 """The fp32 sampler against the reference's fp64 FSM on the sampler's own
 workload (north_star: "travel-time fields match reference fsm3d to a stated
-fp32 tolerance").
+fp32 tolerance"), and what fp32 costs the chains.
 
 The stated bound is
 
-    |u32 - u64| <= 1e-6 * u64 + 1e-7 s     at every node,
+    |u32 - u64| <= 4e-6 * u64 + 4e-7 s     at every node,
 
-u32 from the GPU's fp32 cell-model path (the kernel instance the sampler
-launches: 16-z steps, LDS cell cache, short sqrt), u64 from the REFERENCE's
-own eikonal3d_serial_driver (fsm3d.f90:28-99,648-693, built into
+four times the largest error observed on the sampler's workloads (SURVEY
+s.8c's rule; round 4 measured max |du|/u 9.56e-7 and |du| 1.80e-6 s at C3).
+u32 comes from the GPU's fp32 cell-model path (the kernel instance the
+sampler launches: 16-z steps, LDS cell cache, short sqrt), u64 from the
+REFERENCE's own eikonal3d_serial_driver (fsm3d.f90:28-99,648-693, built into
 oracle/_ref/libfsm3d_ref.so; the fp64 oracle, bitwise equal to it on every
 golden, stands in when the .so is absent) on the same model expanded to fp64
 slowness 1/(double)v per inversion cell.  Checked on full fields and at the
-event nodes the sampler reads, at C3 (128^3, the bench's geometry: chains 0,
-511 and 1023, all 32 stations) and C5 (256^3, where paths are twice as long).
+event nodes the sampler reads:
+
+* C3 (128^3, the bench's geometry and picks): chains 0, 511 and 1023 x all 32
+  stations, on their initial models AND on their models after the bench's 25
+  steps (5 warm-up + 20 timed, bench.py's sigma and dvmax; chains are keyed by
+  global id, so a one-chain sampler at offset c walks chain c of the bench);
+* C5 (256^3, paths twice as long): chain 0 x 8 stations spread over the array.
+
 The logL difference between the sampler's fp32 tables and the reference
 pipeline's tables (fp64 solve exported to fp32, fsm3d.f90:1855-1875) is
-reported.  Observed maxima print as "TOLERANCE ..." lines (run with -s).
+reported, and the fp32 and fp64 samplers are run side by side from the same
+seed at C2 (256 chains, 20 steps) to count identical accept decisions.
+Observed maxima print as "TOLERANCE ..." / "ACCEPT ..." lines (run with -s).
 """
 import os
 
@@ -29,7 +39,8 @@ import _refsolve as R
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-TOL_REL, TOL_ABS = 1e-6, 1e-7
+TOL_REL, TOL_ABS = 4e-6, 4e-7
+BENCH_SIGMA, BENCH_STEPS = 5e-4, 25           # bench.py --sigma default; --warmup 5 + --steps 20 (the driver's run)
 
 
 def _dev():
@@ -69,9 +80,11 @@ def _reference_fields(p, jobs):
 
 
 def _excess(u32, u64):
+    """(max |du| s, max |du|/u, max of |du| - bound, max of |du| / bound)."""
     u32 = np.asarray(u32, dtype=np.float64)
     d = np.abs(u32 - u64)
-    return d.max(), (d / np.maximum(u64, 1e-30)).max(), (d - (TOL_REL * u64 + TOL_ABS)).max()
+    bound = TOL_REL * u64 + TOL_ABS
+    return d.max(), (d / np.maximum(u64, 1e-30)).max(), (d - bound).max(), (d / bound).max()
 
 
 def _gpu_fields(p, vcells, stations, dev):
@@ -89,15 +102,62 @@ def _gpu_fields(p, vcells, stations, dev):
     return u, tt
 
 
+def _check_models(p, label, chains, models, dev, sampler_tabs=None, logls=None):
+    """Full fields and event times of `models` x every station within the
+    bound of the reference; with `sampler_tabs` the sampler's own tables are
+    the batched fields at the event nodes bit for bit.  Prints the maxima
+    first, then asserts."""
+    stations = np.arange(p.nstat)
+    u32, tt32 = _gpu_fields(p, models, stations, dev)
+    if sampler_tabs is not None:
+        for m in range(len(chains)):
+            assert np.array_equal(tt32[m].view(np.uint32), sampler_tabs[m].view(np.uint32)), chains[m]
+    u64, who = _reference_fields(p, [(models[m], s) for m in range(len(chains)) for s in stations])
+    P = O.make_problem(p)
+    ev = p.ev_node
+    worst_f = worst_e = (0.0, 0.0, -1.0, 0.0)
+    fails = []
+    for m, c in enumerate(chains):
+        tt64 = np.empty((p.nstat, p.nevents), np.float32)
+        for s in stations:
+            ref = u64[m * p.nstat + s]
+            f = _excess(u32[m, s], ref)
+            e = _excess(tt32[m, s], ref[ev])
+            if f[2] > 0.0 or e[2] > 0.0:
+                fails.append((c, int(s), f, e))
+            worst_f = max(worst_f, f, key=lambda t: t[3])
+            worst_e = max(worst_e, e, key=lambda t: t[3])
+            tt64[s] = ref[ev].astype(np.float32)          # the reference's fp64 -> fp32 table export
+        l32 = O.loglik(P, tt32[m])
+        l64 = O.loglik(P, tt64)
+        if logls is not None:
+            assert logls[m] == l32, c
+        print(f"TOLERANCE {label} chain {c}: logL fp32 tables {l32:.9f}, reference tables {l64:.9f}, "
+              f"|dlogL| {abs(l32 - l64):.3e} ({abs(l32 - l64) / abs(l64):.3e} relative)")
+    print(f"TOLERANCE {label} fields ({who}): max |du| {worst_f[0]:.3e} s, max |du|/u {worst_f[1]:.3e}, "
+          f"largest |du| / bound {worst_f[3]:.3f} (bound {TOL_REL:g} u + {TOL_ABS:g}); event nodes: "
+          f"max |du| {worst_e[0]:.3e} s, max |du|/u {worst_e[1]:.3e}, |du| / bound {worst_e[3]:.3f}")
+    assert not fails, fails[:4]
+    return worst_f, worst_e
+
+
+def _bench_problem(config):
+    """bench.py's problem: geometry, start models and picks (GPU forward +
+    N(0, sigma), varObs = sigma^2)."""
+    from mceik_amd import mcmc
+    p = mcmc.make_problem(config, picks="analytic")
+    return mcmc.bench_picks(p, BENCH_SIGMA, 0)
+
+
 @pytest.mark.timeout(900)
 def test_c3_sampler_fields_within_fp32_tolerance_of_reference():
     """C3 (the bench's geometry and picks): chains 0, 511, 1023 x all 32
-    stations.  The sampler's own tables equal the batched fields at the event
-    nodes bit for bit; every node of every field and every event time is
-    within the bound of the reference's fp64 solve."""
+    stations on their initial models.  The sampler's own tables equal the
+    batched fields at the event nodes bit for bit; every node of every field
+    and every event time is within the bound of the reference's fp64 solve."""
     dev = _dev()
     from mceik_amd import mcmc
-    p = mcmc.make_problem("C3", picks=mcmc.picks_from_forward(0))
+    p = _bench_problem("C3")
     chains = (0, 511, 1023)
     v0, logl0, ttab = [], [], []
     for c in chains:
@@ -106,38 +166,38 @@ def test_c3_sampler_fields_within_fp32_tolerance_of_reference():
         tt, _, _ = s.last()
         s.close()
         v0.append(v[0]); logl0.append(lg[0]); ttab.append(tt[0])
-    stations = np.arange(p.nstat)
-    u32, tt32 = _gpu_fields(p, v0, stations, dev)
-    for m in range(len(chains)):
-        assert np.array_equal(tt32[m].view(np.uint32), ttab[m].view(np.uint32)), chains[m]
-    u64, who = _reference_fields(p, [(v0[m], s) for m in range(len(chains)) for s in stations])
-    P = O.make_problem(p)
-    ev = p.ev_node
-    worst_f = worst_e = (0.0, 0.0, -1.0)
-    for m, c in enumerate(chains):
-        tt64 = np.empty((p.nstat, p.nevents), np.float32)
-        for s in stations:
-            ref = u64[m * p.nstat + s]
-            f = _excess(u32[m, s], ref)
-            e = _excess(ttab[m][s], ref[ev])
-            assert f[2] <= 0.0, (c, s, f)
-            assert e[2] <= 0.0, (c, s, e)
-            worst_f = max(worst_f, f, key=lambda t: t[1])
-            worst_e = max(worst_e, e, key=lambda t: t[1])
-            tt64[s] = ref[ev].astype(np.float32)          # the reference's fp64 -> fp32 table export
-        l64 = O.loglik(P, tt64)
-        assert logl0[m] == O.loglik(P, ttab[m])
-        print(f"TOLERANCE C3 chain {c}: logL fp32 tables {logl0[m]:.9f}, reference tables {l64:.9f}, "
-              f"|dlogL| {abs(logl0[m] - l64):.3e} ({abs(logl0[m] - l64) / abs(l64):.3e} relative)")
-    print(f"TOLERANCE C3 fields ({who}): max |du| {worst_f[0]:.3e} s, max |du|/u {worst_f[1]:.3e} "
-          f"(bound 1e-6 u + 1e-7); event nodes: max |du| {worst_e[0]:.3e} s, max |du|/u {worst_e[1]:.3e}")
+    _check_models(p, "C3 init", chains, v0, dev, sampler_tabs=ttab, logls=logl0)
 
 
 @pytest.mark.timeout(900)
+def test_c3_fields_after_bench_steps_within_fp32_tolerance():
+    """The same chains after the bench's 25 steps (its sigma and dvmax): the
+    models have moved away from their start (cell contrasts up to +-dvmax per
+    accepted step) and the bound still holds at every node."""
+    dev = _dev()
+    from mceik_amd import mcmc
+    p = _bench_problem("C3")
+    chains = (0, 511, 1023)
+    models, moved = [], []
+    for c in chains:
+        s = mcmc.Sampler(p, nchains=1, chain_offset=c)
+        v0, _, _, _ = s.state()
+        s.run(BENCH_STEPS)
+        v, _, nacc, step = s.state()
+        s.close()
+        assert step == BENCH_STEPS
+        models.append(v[0])
+        moved.append((int((v[0] != v0[0]).sum()), int(nacc[0])))
+    print(f"TOLERANCE C3 after {BENCH_STEPS} steps: (cells changed, accepts) per chain {moved}")
+    assert all(m[0] > 0 for m in moved)
+    _check_models(p, f"C3 step {BENCH_STEPS}", chains, models, dev)
+
+
+@pytest.mark.timeout(1200)
 def test_c5_fields_within_fp32_tolerance_of_reference():
-    """C5 (256^3, paths twice C3's): chain 0's cell model, stations 0 and 1:
-    full fields and the sampler's event times within the bound of the
-    reference's fp64 solve."""
+    """C5 (256^3, paths twice C3's): chain 0's cell model, 8 stations spread
+    over the array: full fields and the sampler's event times within the
+    bound of the reference's fp64 solve."""
     dev = _dev()
     torch.cuda.empty_cache()
     from mceik_amd import mcmc
@@ -147,14 +207,61 @@ def test_c5_fields_within_fp32_tolerance_of_reference():
     ttab, _, _ = s.last()
     s.close()
     torch.cuda.empty_cache()
-    stations = np.array([0, 1])
-    u32, tt32 = _gpu_fields(p, [v[0]], stations, dev)
-    assert np.array_equal(tt32[0].view(np.uint32), ttab[0, :2].view(np.uint32))
+    stations = np.arange(0, p.nstat, p.nstat // 8)[:8]
+    worst = (0.0, 0.0, -1.0, 0.0)
     u64, who = _reference_fields(p, [(v[0], s) for s in stations])
-    for k, st in enumerate(stations):
-        f = _excess(u32[0, k], u64[k])
-        e = _excess(ttab[0, st], u64[k][p.ev_node])
-        print(f"TOLERANCE C5 station {st} ({who}): max |du| {f[0]:.3e} s, max |du|/u {f[1]:.3e}; "
-              f"event nodes max |du|/u {e[1]:.3e}")
-        assert f[2] <= 0.0, (st, f)
-        assert e[2] <= 0.0, (st, e)
+    fails = []
+    for half in (stations[:4], stations[4:]):            # 4 fields of 64 MiB at a time
+        u32, tt32 = _gpu_fields(p, [v[0]], half, dev)
+        assert np.array_equal(tt32[0].view(np.uint32), ttab[0, half].view(np.uint32))
+        for k, st in enumerate(half):
+            ref = u64[int(np.flatnonzero(stations == st)[0])]
+            f = _excess(u32[0, k], ref)
+            e = _excess(ttab[0, st], ref[p.ev_node])
+            print(f"TOLERANCE C5 station {st} ({who}): max |du| {f[0]:.3e} s, max |du|/u {f[1]:.3e}, "
+                  f"|du| / bound {f[3]:.3f}; event nodes max |du|/u {e[1]:.3e}")
+            worst = max(worst, f, key=lambda t: t[3])
+            if f[2] > 0.0 or e[2] > 0.0:
+                fails.append((int(st), f, e))
+        del u32
+        torch.cuda.empty_cache()
+    print(f"TOLERANCE C5 fields: max |du|/u {worst[1]:.3e}, largest |du| / bound {worst[3]:.3f}")
+    assert not fails, fails
+
+
+ACCEPT_FLOOR = 0.99          # identical accept decisions, fp32 vs fp64 sampler
+
+
+@pytest.mark.timeout(900)
+def test_c2_fp32_and_fp64_samplers_accept_alike():
+    """What fp32 costs the chain: the fp32 sampler (the headline) and the fp64
+    sampler (the reference's arithmetic, fsm3d.f90:624-693) run from the same
+    seed, start models and bench picks at C2 (256 chains, 20 steps).  Reports
+    the fraction of identical accept decisions, the chains whose whole accept
+    sequence agrees and the first divergent (chain, step); asserts the
+    stated floor on identical decisions."""
+    _dev()
+    from mceik_amd import mcmc
+    p = _bench_problem("C2")
+    nch, nsteps = 256, 20
+    acc = {}
+    for prec in (32, 64):
+        s = mcmc.Sampler(p, nchains=nch, precision=prec)
+        seq = []
+        for _ in range(nsteps):
+            s.run(1)
+            seq.append(s.last()[2].astype(bool).copy())
+        acc[prec] = np.array(seq)                            # [step, chain]
+        s.close()
+    same = acc[32] == acc[64]
+    frac = float(same.mean())
+    chains_same = float(same.all(axis=0).mean())
+    bad = np.argwhere(~same)
+    first = None
+    if len(bad):
+        k = int(np.argmin(bad[:, 0] * nch + bad[:, 1]))
+        first = (int(bad[k, 1]), int(bad[k, 0]))           # (chain, step)
+    print(f"ACCEPT C2 fp32 vs fp64 sampler, {nch} chains x {nsteps} steps: identical decisions {frac:.5f} "
+          f"({int((~same).sum())} differ), chains with identical sequences {chains_same:.4f}, first divergence "
+          f"(chain, step) {first}; accept rate fp32 {acc[32].mean():.3f} fp64 {acc[64].mean():.3f}")
+    assert frac >= ACCEPT_FLOOR
