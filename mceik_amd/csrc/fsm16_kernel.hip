@@ -47,9 +47,12 @@ struct Smem16 {
     unsigned short *lastchg;     //   ... of the last visit that changed it
     int *ring_e, *ring_b;        // per position (mod nr): entry tx | ty << 12 | tz << 24 (bubble -1), block id
     unsigned *ring_base;         //   ... byte offset of the tile's line groups
+    unsigned *fmask;             //   ... held stream: what the visit changed (H16_OWN | face bits) | H16_CONT
     int *scratch;                // visit statistics / traffic counters
     float *xr;                   // neighbour rows XR [4][80][4], then XN (same shape)
     unsigned *meta;              // [nr][64] column meta (flags | tz << 9 | cell-cache base << 16)
+    unsigned char *fz;           // held stream: per tile, the z-blocks decided in this sweep (sweep z order)
+    unsigned *vbits, *cbits;     // held stream: blocks visited / changed in this iteration (bitmaps)
 };
 template <bool FIXED>
 __device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char *base)
@@ -58,7 +61,9 @@ __device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char 
     if (FIXED) {         // fsm16_fixed_layout(): constants (checked on the host)
         off[8] = F16_CINFO; off[7] = F16_XR; off[1] = F16_CC; off[5] = F16_RING; off[6] = F16_SCRATCH;
         off[3] = F16_LASTPROC; off[4] = F16_LASTCHG; off[2] = F16_ORDER;
-        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 2);
+        off[9] = F16_ORDER + mceik_align16((size_t)L.ntiles * 2);
+        off[10] = off[9] + mceik_align16((size_t)L.ntiles);
+        off[0] = off[10] + f16_bitmap_bytes(L);
     } else {
         fsm16_smem_layout(L, off);
     }
@@ -72,6 +77,10 @@ __device__ __forceinline__ Smem16 smem16_bind(const FsmLaunch &L, unsigned char 
     S.ring_e = reinterpret_cast<int *>(base + off[5]);
     S.ring_b = S.ring_e + (FIXED ? F16_NR : nr);
     S.ring_base = reinterpret_cast<unsigned *>(S.ring_b + (FIXED ? F16_NR : nr));
+    S.fmask = S.ring_base + (FIXED ? F16_NR : nr);
+    S.fz = base + off[9];
+    S.vbits = reinterpret_cast<unsigned *>(base + off[10]);
+    S.cbits = S.vbits + (L.nblocks + 31) / 32;
     S.scratch = reinterpret_cast<int *>(base + off[6]);
     S.xr = reinterpret_cast<float *>(base + off[7]);
     S.meta = reinterpret_cast<unsigned *>(base + off[8]);
@@ -129,6 +138,19 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 #ifndef MCEIK16_NPASS
 #define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
 #endif
+#ifndef MCEIK16_HOLD
+#define MCEIK16_HOLD 1           // the held stream (decide16h): face-level change marks, blocks with an
+                                 // in-flight dependency and no settled reason wait instead of being visited
+#endif
+// held stream: the per-position change mask (Smem16.fmask), bit 0 the block changed, bits 1-6 the face
+// layer it changed (x-low, x-high, y-low, y-high, z-low, z-high; absolute orientation), and H16_CONT:
+// the next position continues this position's z-run (same tile, next block in sweep z order)
+#define H16_OWN 1u
+#define H16_CONT 256u
+// BInfo16.w1 bit 24: the brick is the last of its position below the column end, so its z-downwind
+// node is loaded from HBM (into the z-boundary register with the run-start node) for a run that
+// does not continue
+#define W1_ZD (1u << 24)
 
 // ---- global loads / stores of 64-B segments ------------------------------
 // Pair-coalesced (lanes 2i, 2i+1 = x neighbours): each instruction makes both
@@ -328,13 +350,14 @@ __device__ __forceinline__ void bload4h(Rsrc r, uint32_t off, float (&v)[4])
 // (signed 16) | position clock << 16; w3 = block id | BC z-slot mask << 16.
 struct BInfo16 {
     uint32_t seg;            // own 64-B segment (OOB if none)
-    uint32_t zh;             // z-upwind node of a run start (prefetch only)
+    uint32_t zh;             // z-boundary node (prefetch only): the z-upwind node of a run start (first
+                             // brick of a position) or the z-downwind node (last brick, W1_ZD)
     uint32_t lseg;           // this brick's half of its column line if the line holds a valid brick
                              // (prefetch only: a line loader whose own brick is past the grid end)
     uint32_t w1, w2, w3;
     __device__ __forceinline__ int fl() const { return (int)(w1 & 0xfffu); }
     __device__ __forceinline__ int zb() const { return (int)((w1 >> 12) & 0xffu); }   // (lean: the phase)
-    __device__ __forceinline__ int ri() const { return (int)(w1 >> 20); }
+    __device__ __forceinline__ int ri() const { return (int)((w1 >> 20) & 0xfu); }
     __device__ __forceinline__ int ccb() const { return (int)(w2 << 16) >> 16; }
     __device__ __forceinline__ int clk() const { return (int)(w2 >> 16); }
     __device__ __forceinline__ int bid() const { return (int)(w3 & 0xffffu); }
@@ -356,6 +379,11 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
     int fl = valid ? (int)((meta & 0x7f) | F_VALID) : 0;
     if (zb == (RZ ? g.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : g.nzb - 1)) fl |= F_LAST;
+    const bool zd = MCEIK16_HOLD && valid && p.zbs == kb - 1 && !(fl & F_LAST);
+    if (zd) {
+        const int zn = RZ ? zb * 16 - 1 : zb * 16 + 16;      // z-downwind node of the brick's last slot
+        b.zh = col + zoff16(zn >> 4) + (uint32_t)(zn & 15) * 4u;
+    }
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
     bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && zb * 16 + 16 > L.nz);
     unsigned bcm = 0;
@@ -379,7 +407,7 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
     }
     if (slow) fl |= F_SLOW;
     const int ccb = ci_ccb(meta) + zb * 4;                     // nrz = 4: cell of node z = base + z / 4
-    b.w1 = (uint32_t)fl | ((uint32_t)(valid ? zb : 0) << 12) | ((uint32_t)p.ri << 20);
+    b.w1 = (uint32_t)fl | ((uint32_t)(valid ? zb : 0) << 12) | ((uint32_t)p.ri << 20) | (zd ? W1_ZD : 0u);
     b.w2 = ((uint32_t)ccb & 0xffffu) | ((uint32_t)p.sp << 16);
     b.w3 = ((uint32_t)S.ring_b[p.ri] & 0xffffu) | (bcm << 16);
     return b;
@@ -439,6 +467,10 @@ __device__ __forceinline__ BInfo16 brick_info_lean(const FsmLaunch &L, const Sme
     b.seg = valid ? off : OOB;
     b.lseg = pv && (w & ((16u << LW_G(0)) | (16u << LW_G(1)))) ? off : OOB;
     b.zh = valid && (gp & 8u) ? off + (RZ ? 8192u - 64u : 124u - 8192u) : OOB;
+    // the last brick of the position below the column end: its z-downwind node (the next line group's
+    // first node, or the previous one's last node when z descends)
+    const bool zd = MCEIK16_HOLD && valid && ph == 1 && !(gp & 2u);
+    if (zd) b.zh = off + (RZ ? 124u - 8192u : 8192u - 64u);
     int fl = valid ? (int)((w & 0x7fu) | F_VALID | ((gp & 15u) << 8)) : 0;
     unsigned bcm = 0;
     if (__any(fl & C_BC)) {
@@ -459,7 +491,7 @@ __device__ __forceinline__ BInfo16 brick_info_lean(const FsmLaunch &L, const Sme
         if (bcm) fl |= F_SLOW;
     }
     const int ccb = (int)(w >> LW_CCB) + (RZ ? -4 * ph : 4 * ph);
-    b.w1 = (uint32_t)fl | ((uint32_t)ph << 12) | ((uint32_t)p.ri << 20);
+    b.w1 = (uint32_t)fl | ((uint32_t)ph << 12) | ((uint32_t)p.ri << 20) | (zd ? W1_ZD : 0u);
     b.w2 = ((uint32_t)ccb & 0xffffu) | ((uint32_t)p.sp << 16);
     b.w3 = ((uint32_t)S.ring_b[p.ri] & 0xffffu) | (bcm << 16);
     return b;
@@ -597,6 +629,243 @@ __device__ __forceinline__ int decide16(const FsmLaunch &L, const Fsm16Geo &g, c
     return e;
 }
 
+// ---- the held stream (MCEIK16_HOLD) ------------------------
+// The z-blocks of a sweep are decided tile by tile in diagonal order, but a
+// tile's blocks one at a time (frontier fz, sweep z order), and a block only
+// once the blocks it reads new values from are decided: its sweep-upwind x and
+// y neighbours (the upwind tiles' frontiers are past it) and its z-below (the
+// frontier).  Then, with clocks relative to the sweep:
+//   need >= lastproc (it changed at its last visit, or a neighbour changed
+//     the face layer it shares with it since: settled marks)  -> visit, once
+//     its upwind visits are >= vis positions back (a z-below visited at the
+//     previous position continues the run in registers);
+//   else an upwind neighbour or the z-below still in flight   -> wait (held);
+//   else                                                      -> skip.
+// A skipped block would recompute every node from unchanged inputs, so
+// skipping is exact, like the block-level rule of decide16 (whose in-flight
+// and run-continuation visits almost never change anything: profiles/r05_admit).
+// A visit's changes are "settled" infl positions after it (every lane is past
+// it): the change mask its lanes collected (Smem16.fmask) then marks need of
+// the block itself and of the neighbours across the faces it changed.
+enum { H16_DONE = 0, H16_BLOCKED, H16_HELD, H16_WAIT, H16_SKIP, H16_READY };
+__device__ __forceinline__ int tile_id16(const FsmLaunch &L, const Smem16 &S, int ti, int rx, int ry)
+{
+    const int o = S.order[ti];
+    const int txs = o & 0xff, tys = o >> 8;
+    return (ry ? L.nty - 1 - tys : tys) * L.ntx + (rx ? L.ntx - 1 - txs : txs);
+}
+template <bool RZ>
+__device__ __forceinline__ int tile_status16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, int ti, int C,
+                                             int rx, int ry, int &id, int &k, int &runon)
+{
+    const int o = S.order[ti];
+    const int txs = o & 0xff, tys = o >> 8;
+    const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+    const int nt = L.ntiles, nzk = L.nzk;
+    id = ty * L.ntx + tx;
+    k = S.fz[id];
+    runon = 0;
+    if (k >= nzk) return H16_DONE;
+    const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
+    const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -1;
+    if ((xu >= 0 && (int)S.fz[xu] <= k) || (yu >= 0 && (int)S.fz[yu] <= k)) return H16_BLOCKED;
+    const int tz = RZ ? nzk - 1 - k : k;
+    const int b = tz * nt + id;
+    const bool reason = S.lastchg[b] >= S.lastproc[b];
+    int dep = -0x40000000;                               // latest upwind visit (this sweep's clocks)
+    if (xu >= 0) dep = max(dep, (int)S.lastproc[tz * nt + xu]);
+    if (yu >= 0) dep = max(dep, (int)S.lastproc[tz * nt + yu]);
+    const int zl = k > 0 ? (int)S.lastproc[b + (RZ ? nt : -nt)] : -0x40000000;
+    runon = zl == C - 1;
+    if (!runon) dep = max(dep, zl);
+    if (reason) return dep + g.vis <= C ? H16_READY : H16_WAIT;
+    return (runon || dep > C - g.infl) ? H16_HELD : H16_SKIP;
+}
+// The block of position C (the previous position's ring slot rprev): the next
+// block of the previous position's tile when it is ready, else the first ready
+// block in diagonal order -- windows of 64 tiles from the first incomplete one,
+// every lane deciding its tile's next block per round, until a block is ready
+// or no lane can skip.  Returns the entry tx | ty << 12 | tz << 24, -1 (a
+// bubble) or -2 (every tile decided: the sweep's stream ends).  Progress: the
+// first incomplete tile's upwind tiles are complete, so within infl positions
+// its next block is ready or skipped.
+struct HoldStream {
+    int done;                    // tiles [0, done) of the diagonal order are complete
+    int last;                    // diagonal index of the previous position's tile, -1 none
+};
+template <bool RZ>
+__device__ __forceinline__ int decide16h(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, HoldStream &st,
+                                         int C, int rx, int ry, int rprev, int &zh)
+{
+    const int lane = threadIdx.x, nt = L.ntiles;
+    zh = 0;
+    int pick = -1, pid = 0, pk = 0, pro = 0;
+    if (st.last >= 0) {
+        int id, k, ro;
+        const int s = tile_status16<RZ>(L, g, S, st.last, C, rx, ry, id, k, ro);
+        if (__builtin_amdgcn_readfirstlane(s) == H16_READY) {
+            pick = st.last;
+            pid = __builtin_amdgcn_readfirstlane(id);
+            pk = __builtin_amdgcn_readfirstlane(k);
+            pro = __builtin_amdgcn_readfirstlane(ro);
+        }
+    }
+    if (pick < 0) {
+        for (;;) {                                   // the complete tiles at the front
+            const int ti = st.done + lane;
+            const bool cpl = ti < nt && (int)S.fz[tile_id16(L, S, ti, rx, ry)] >= L.nzk;
+            const unsigned long long m = ~__ballot(cpl);
+            const int n = m ? __builtin_ctzll(m) : 64;
+            st.done += n;
+            if (n < 64) break;
+        }
+        if (st.done >= nt) {
+            st.last = -1;
+            return -2;
+        }
+        for (int base = st.done; base < nt && pick < 0; base += 64) {
+            const int ti = base + lane;
+            for (;;) {
+                int s = H16_DONE, id = 0, k = 0, ro = 0;
+                if (ti < nt) s = tile_status16<RZ>(L, g, S, ti, C, rx, ry, id, k, ro);
+                const bool sk = s == H16_SKIP;
+                if (sk) S.fz[id] = (unsigned char)(k + 1);
+                const unsigned long long rm = __ballot(s == H16_READY);
+                if (rm) {
+                    const int f = __builtin_ctzll(rm);
+                    pick = base + f;
+                    pid = __builtin_amdgcn_readfirstlane(__shfl(id, f, 64));
+                    pk = __builtin_amdgcn_readfirstlane(__shfl(k, f, 64));
+                    pro = __builtin_amdgcn_readfirstlane(__shfl(ro, f, 64));
+                    break;
+                }
+                if (!__ballot(sk)) break;
+                asm volatile("" ::: "memory");       // this round's frontiers feed the next
+            }
+        }
+    }
+    if (pick < 0) {
+        st.last = -1;
+        return -1;
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0) {
+        S.fz[pid] = (unsigned char)(pk + 1);
+        if (pro) atomicOr(&S.fmask[rprev], H16_CONT);   // the previous position's run continues here
+    }
+    asm volatile("" ::: "memory");
+    st.last = pick;
+    zh = pk > 0 && !pro;                             // a run start above the column's first block
+    const int ty = pid / L.ntx, tx = pid - ty * L.ntx;
+    return tx | (ty << 12) | ((RZ ? L.nzk - 1 - pk : pk) << 24);
+}
+// Settle the visit of ring slot ri (clock clk): its change mask marks need of
+// the block (and the iteration's changed bitmap) and of the neighbours across
+// the changed faces; lanes 0-6 take one target each.
+__device__ __forceinline__ void settle16h(const FsmLaunch &L, const Smem16 &S, int ri, int clk)
+{
+    const int lane = threadIdx.x;
+    asm volatile("" ::: "memory");
+    const int e = S.ring_e[ri];
+    const unsigned m = S.fmask[ri];
+    if (e >= 0 && lane < 7 && ((m >> lane) & 1u)) {
+        const int tx = e & 0xfff, ty = (e >> 12) & 0xfff, tz = (e >> 24) & 0xff;
+        const int nt = L.ntiles, b = tz * nt + ty * L.ntx + tx;
+        const int t = lane == 0 ? b
+                    : lane == 1 ? (tx > 0 ? b - 1 : -1)
+                    : lane == 2 ? (tx < L.ntx - 1 ? b + 1 : -1)
+                    : lane == 3 ? (ty > 0 ? b - L.ntx : -1)
+                    : lane == 4 ? (ty < L.nty - 1 ? b + L.ntx : -1)
+                    : lane == 5 ? (tz > 0 ? b - nt : -1)
+                    : (tz < L.nzk - 1 ? b + nt : -1);
+        if (t >= 0) S.lastchg[t] = (unsigned short)clk;
+        if (lane == 0) S.cbits[b >> 5] |= 1u << (b & 31);
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0) S.fmask[ri] = 0;
+    asm volatile("" ::: "memory");
+}
+// Start of a held sweep: every block's pending state (need >= lastproc)
+// becomes need 1 / 0 against lastproc 1, the frontiers restart, and the
+// sweep's clock starts at 64 (a sweep needs at most nblocks (1 + infl) + 64
+// < 2^16 clocks: between two visits at most infl bubbles).
+__device__ __forceinline__ void norm16h(const FsmLaunch &L, const Smem16 &S)
+{
+    asm volatile("" ::: "memory");
+    for (int b = threadIdx.x; b < L.nblocks; b += 64) {
+        const bool pend = S.lastchg[b] >= S.lastproc[b];
+        S.lastproc[b] = 1;
+        S.lastchg[b] = pend ? 1 : 0;
+    }
+    for (int t = threadIdx.x; t < L.ntiles; t += 64) S.fz[t] = 0;
+    asm volatile("" ::: "memory");
+}
+
+#ifdef MCEIK_ADMIT_STATS
+// Experiment build (-DMCEIK_TRAFFIC -DMCEIK_ADMIT_STATS; the traffic
+// counters then hold admission statistics instead of bytes): why each
+// admitted z-block was visited -- 1 it changed at its last visit, 2 a face
+// neighbour changed since, 3 only its upwind x/y neighbour is in flight,
+// 4 none of these (the continuation of a z-run) -- counted in [reason - 1],
+// and in [3 + reason] when the visit changed the block.  A slot's previous
+// position is settled when the slot is reused (nr positions later: every
+// lane is past it) or at the end of the sweep (admit_flush16).
+__device__ __forceinline__ void admit_settle16(const Smem16 &S, int ri)
+{
+    const int r = S.scratch[16 + ri];
+    if (r) {
+        const int b = S.ring_b[ri];
+        S.scratch[8 + r - 1] += 1;
+        if (S.lastchg[b] == S.lastproc[b]) S.scratch[8 + 3 + r] += 1;
+        S.scratch[16 + ri] = 0;
+    }
+}
+__device__ __forceinline__ void admit_account16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, int entry,
+                                                int ri, int C, int rx, int ry)
+{
+    asm volatile("" ::: "memory");
+    if (threadIdx.x == 0) {
+        admit_settle16(S, ri);
+        if (entry >= 0) {
+            const int nt = L.ntiles;
+            const int tz = (entry >> 24) & 0xff, tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
+            const int id = ty * L.ntx + tx, b = tz * nt + id;
+            const int txs = rx ? L.ntx - 1 - tx : tx, tys = ry ? L.nty - 1 - ty : ty;
+            const int lp = S.lastproc[b];
+            int r = 4;
+            if (S.lastchg[b] >= lp) {
+                r = 1;
+            } else {
+                bool d = false;
+                if (tx > 0) d |= S.lastchg[b - 1] > lp;
+                if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
+                if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
+                if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
+                if (tz > 0) d |= S.lastchg[b - nt] > lp;
+                if (tz < L.nzk - 1) d |= S.lastchg[b + nt] > lp;
+                if (d) {
+                    r = 2;
+                } else {
+                    bool f = false;
+                    if (txs > 0) f |= (int)S.lastproc[tz * nt + id + (rx ? 1 : -1)] > C - g.infl;
+                    if (tys > 0) f |= (int)S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)] > C - g.infl;
+                    if (f) r = 3;
+                }
+            }
+            S.scratch[16 + ri] = r;
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void admit_flush16(const Smem16 &S, int nr)
+{
+    asm volatile("" ::: "memory");
+    if (threadIdx.x == 0)
+        for (int ri = 0; ri < nr; ri++) admit_settle16(S, ri);
+    asm volatile("" ::: "memory");
+}
+#endif
+
 // Admit position (ring slot ri, relative clock C): every lane writes its
 // column meta, lane 0 the ring entry, block id, tile base and the block's
 // visit clock.  u0 flag: the block's first visit in this iteration
@@ -609,11 +878,16 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
     unsigned meta = 0;
     int bid = 0, nbv = 0;
     uint32_t base = 0;
+#if defined(MCEIK_ADMIT_STATS) && !MCEIK16_HOLD
+    admit_account16(L, g, S, entry, ri, C, rx, ry);
+#endif
     if (entry >= 0) {
         const int tz = (entry >> 24) & 0xff, tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
         bid = tz * L.ntiles + tx + ty * L.ntx;
         nbv = min(L.kb, L.nzb - tz * L.kb);          // 8-z bricks of the block (visit statistics)
-        const int u0flag = S.lastproc[bid] < 64;       // no visit since the iteration started (clock 64)
+        // no visit since the iteration started (clock 64; the held stream's clocks restart every
+        // sweep, so there the iteration's visits are a bitmap)
+        const int u0flag = MCEIK16_HOLD ? !((S.vbits[bid >> 5] >> (bid & 31)) & 1u) : S.lastproc[bid] < 64;
         if ((entry & 0xffffff) != ct.tile) column_tile<float>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         meta = LEAN ? lean_word<RZ>(L, g, ct, tz, ri, u0flag, zh) : column_word(L, L.kb, ct, tz, ri, u0flag, zh);
         base = (uint32_t)(ty * L.ntx + tx) * tile_bytes<float>(L) + (LEAN ? (uint32_t)tz << 13 : 0u);
@@ -624,6 +898,7 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
     if (threadIdx.x == 0) {
         if (entry >= 0) {
             S.lastproc[bid] = (unsigned short)C;
+            if (MCEIK16_HOLD) S.vbits[bid >> 5] |= 1u << (bid & 31);
             if (L.visit_stats) {
                 S.scratch[0] += nbv;
                 S.scratch[1] += nbv * nact;
@@ -677,7 +952,7 @@ __device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
 template <bool RZ, bool GENERIC, bool LEAN>
 __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, const BInfo16 &b0, float (&v)[16],
                                         float zprev0, float znext, int lx, int ly, int rx, int ry, bool &changed,
-                                        bool &nc, int &ierr_last)
+                                        bool &nc, int &ierr_last, bool &c0, bool &c15)
 {
     const int lane = threadIdx.x;
     const float T = (float)L.conv_thresh;
@@ -761,6 +1036,8 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
             const bool dec = nv < self;
             nc |= dec && self >= T;
             changed |= dec;
+            if (pj == 0) c0 = dec;                          // the brick's lowest / highest node changed
+            if (pj == 15) c15 = dec;                        //   (z faces of its block, held stream)
             v[pj] = nv;
         }
     }
@@ -793,6 +1070,27 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
 
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
+    constexpr bool HOLD = MCEIK16_HOLD;
+    HoldStream hs_;
+    hs_.done = 0; hs_.last = -1;
+    int nset = 0;                                    // held stream: positions settled so far
+    // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
+    // lane's column is a tile edge (absolute orientation)
+    const unsigned xyface = H16_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
+                            (ly == 7 ? 16u : 0u);
+    if (HOLD) {
+        norm16h(L, S);
+        clock0 = 64;
+    }
+    // the next position's block (held stream: after settling the visit infl positions back)
+    auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
+        if (!HOLD) return decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
+        while (nset <= pos - g.infl) {
+            settle16h(L, S, nset % nr, clock0 + nset);
+            nset++;
+        }
+        return decide16h<RZ>(L, g, S, hs_, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, zh);
+    };
     constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
     constexpr bool LEAN = KB16 == 2 && MCEIK16_LEAN;     // lean position words (2-step positions)
     // ping-pong register sets by step parity (the step loop runs in pairs, so
@@ -825,7 +1123,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     int ndecided = 0, nstream = 0x7fffffff, dri = 0;
     for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
         int zh;
-        const int e = decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
+        const int e = decide_any(pos, dri, zh);
         if (e == -2) {
             if (pos == 0) return 0;                         // nothing changed near any block: skip the sweep
             nstream = pos;
@@ -964,7 +1262,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         if (ph == 0 && nstream == 0x7fffffff) {
             const int pos = ndecided;
             int zh;
-            const int e = decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
+            const int e = decide_any(pos, dri, zh);
             if (e == -2) {
                 nstream = pos;
             } else {
@@ -1033,13 +1331,20 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         }
         // ---- the 16 z-slots of the current brick (next brick's first value
         // in sweep order from this lane's XN row)
-        const float znext = S.xr[XROW16(1, RZ ? 3 : 0, lane) + (RZ ? 3 : 0)];
+        float znext = S.xr[XROW16(1, RZ ? 3 : 0, lane) + (RZ ? 3 : 0)];
+        unsigned fmk = 0;
+        if (HOLD) {
+            // the position's last brick: its z-downwind node is the next brick's first (XN row) only
+            // when the run continues, else the node loaded from HBM
+            fmk = S.fmask[b0.ri()];
+            if ((b0.w1 & W1_ZD) && !(fmk & H16_CONT)) znext = zc;
+        }
         const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
-        bool changed = false, nc = false;
+        bool changed = false, nc = false, c0 = false, c15 = false;
         if (__any(b0.fl() & F_SLOW))
-            brick16<RZ, true, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
+            brick16<RZ, true, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
         else
-            brick16<RZ, false, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last);
+            brick16<RZ, false, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
 #ifdef MCEIK_EXP_VALU
         {   // sensitivity experiment: N extra dependent VALU per step (results unchanged)
             unsigned x = (unsigned)B;
@@ -1116,7 +1421,17 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             }
         }
         TRAF(S, 3, changed, 64);
-        if (changed) S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
+        if (HOLD) {
+            // what this lane changed: the block, its x / y faces (edge columns), its z faces (the
+            // block's lowest / highest node of the column)
+            if (changed) {
+                const int zr = LEAN ? (b0.zb() ^ (RZ ? 1 : 0)) : b0.zb() % kb;   // brick index in the block
+                const unsigned m = xyface | ((zr == 0 && c0) ? 32u : 0u) | ((zr == kb - 1 && c15) ? 64u : 0u);
+                atomicOr(&S.fmask[b0.ri()], m);
+            }
+        } else if (changed) {
+            S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
+        }
         load_row16(S.xr, 1, lane, v);
         if (FL) {
             line_write(S.xr, lq, hpcur);
@@ -1145,6 +1460,13 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         }
     }
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
+    if (HOLD) {
+        // the last visits' changes (every lane is past them)
+        for (; nset < nstream; nset++) settle16h(L, S, nset % nr, clock0 + nset);
+    }
+#if defined(MCEIK_ADMIT_STATS) && !MCEIK16_HOLD
+    admit_flush16(S, nr);
+#endif
     return nstream;
 }
 
@@ -1157,7 +1479,8 @@ __device__ __forceinline__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, 
     const float T = (float)L.conv_thresh, tolr = (float)L.tol;
     for (int base = 0; base < L.nblocks; base += 64) {
         const int k = base + lane;
-        const bool flag = k < L.nblocks && S.lastchg[k] >= 64;
+        const bool flag = k < L.nblocks && (MCEIK16_HOLD ? ((S.cbits[k >> 5] >> (k & 31)) & 1u) != 0
+                                                         : S.lastchg[k] >= 64);
         unsigned long long m = __ballot(flag);
         while (m) {
             const int bid = base + __builtin_ctzll(m);
@@ -1396,10 +1719,14 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         for (int t = lane; t < L.nblocks; t += 64) {
             S.lastproc[t] = 2; S.lastchg[t] = 1;
         }
+        if (MCEIK16_HOLD && lane < g.nr) S.fmask[lane] = 0;
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
 #ifdef MCEIK_TRAFFIC
         if (lane == 0)
             for (int k = 0; k < MCEIK_TRAFFIC_N; k++) S.scratch[8 + k] = 0;
+#endif
+#ifdef MCEIK_ADMIT_STATS
+        if (lane < 16) S.scratch[16 + lane] = 0;
 #endif
         unsigned nchg = 0, nsteps = 0;
         BcBoxes bc;
@@ -1410,8 +1737,20 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
                 const int *q = bc.box + 6 * k;
                 for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
                     for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
-                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
-                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = 3;
+                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++) {
+                            const int b = (tz * L.nty + ty) * L.ntx + tx;
+                            S.lastchg[b] = 3;
+                            if (MCEIK16_HOLD) {
+                                // (the held stream marks neighbours only through need: every face
+                                // of a boundary-condition block counts as changed)
+                                if (tx > 0) S.lastchg[b - 1] = 3;
+                                if (tx < L.ntx - 1) S.lastchg[b + 1] = 3;
+                                if (ty > 0) S.lastchg[b - L.ntx] = 3;
+                                if (ty < L.nty - 1) S.lastchg[b + L.ntx] = 3;
+                                if (tz > 0) S.lastchg[b - L.ntiles] = 3;
+                                if (tz < L.nzk - 1) S.lastchg[b + L.ntiles] = 3;
+                            }
+                        }
             }
         }
         asm volatile("" ::: "memory");
@@ -1420,7 +1759,13 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
-                iter_norm(L, S);
+                if (MCEIK16_HOLD) {
+                    // (the held stream rebases its clocks every sweep, norm16h)
+                    for (int w = lane; w < (L.nblocks + 31) / 32; w += 64) { S.vbits[w] = 0; S.cbits[w] = 0; }
+                    asm volatile("" ::: "memory");
+                } else {
+                    iter_norm(L, S);
+                }
                 int clock = 64;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;

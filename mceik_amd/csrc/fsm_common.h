@@ -92,7 +92,9 @@ static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b
 // Debug / accounting counters in LDS: [0..3] visit statistics; MCEIK_TRAFFIC
 // builds add [8..15], the requested global-memory bytes of the wave's current
 // sweep by category (flushed to FsmLaunch.traffic after every sweep).
-#ifdef MCEIK_TRAFFIC
+#if defined(MCEIK_ADMIT_STATS)
+#define MCEIK_SCRATCH_BYTES 128  // + [16..31]: admission reason of each ring slot's position
+#elif defined(MCEIK_TRAFFIC)
 #define MCEIK_SCRATCH_BYTES 64
 #else
 #define MCEIK_SCRATCH_BYTES 32
@@ -217,10 +219,13 @@ static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t
 }
 // LDS of one fsm16 solve wave: 0 BC boxes | 1 cell cache [nr][ccb] float | 2 tile order int [ntiles] |
 // 2 is u16 (txs | tys << 8) | 3 lastproc u16 [nblocks] | 4 lastchg u16 [nblocks] (clocks relative to the
-// iteration) |
-// 5 ring: entry int [nr], block id int [nr], tile base u32 [nr] | 6 scratch |
-// 7 neighbour rows XR then XN, each [4 quarters][80 rows][4] float | 8 column meta u32 [nr][64]
-#define MCEIK_SMEM16_ARRAYS 9
+// iteration; with the held stream, MCEIK16_HOLD: relative to the sweep, and lastchg holds
+// "need", the clock of the last settled change of the block or of a neighbour's face it shares) |
+// 5 ring: entry int [nr], block id int [nr], tile base u32 [nr], change mask u32 [nr] | 6 scratch |
+// 7 neighbour rows XR then XN, each [4 quarters][80 rows][4] float | 8 column meta u32 [nr][64] |
+// 9 tile frontier u8 [ntiles] (z-blocks decided in this sweep) | 10 two block bitmaps u32 [nblocks / 32]
+// (visited / changed in this iteration)
+#define MCEIK_SMEM16_ARRAYS 11
 // floats per quarter array of the neighbour rows: 80 rows of 4 plus a 16-B pad,
 // so that the x-pair exchange (even lane: quarter 0, odd lane: quarter 1 of the
 // same row) falls in different LDS banks (unpadded, 320 floats = 5 x 64 banks)
@@ -233,7 +238,7 @@ static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t
 #define F16_XR (F16_CINFO + F16_NR * 64 * 4)
 #define F16_CC (F16_XR + 2 * 4 * MCEIK_X16Q * 4)
 #define F16_RING (F16_CC + F16_NR * 32 * 4)
-#define F16_SCRATCH (F16_RING + 128)
+#define F16_SCRATCH (F16_RING + 176)
 #define F16_LASTPROC (F16_SCRATCH + MCEIK_SCRATCH_BYTES)
 #define F16_LASTCHG (F16_LASTPROC + MCEIK_MAX_BLOCKS * 2)
 #define F16_ORDER (F16_LASTCHG + MCEIK_MAX_BLOCKS * 2)
@@ -241,13 +246,19 @@ static inline __host__ __device__ bool fsm16_fixed_layout(const FsmLaunch &L)
 {
     return fsm16_eligible(L, 4) && L.kb == 4 && L.ccb <= 32 && fsm16_geo(L).nr == F16_NR;
 }
+static inline __host__ __device__ size_t f16_bitmap_bytes(const FsmLaunch &L)
+{
+    return mceik_align16((size_t)((L.nblocks + 31) / 32) * 4 * 2);
+}
 static inline __host__ __device__ size_t fsm16_smem_layout(const FsmLaunch &L, size_t *off)
 {
     const size_t nbox = mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
     if (fsm16_fixed_layout(L)) {
         off[8] = F16_CINFO; off[7] = F16_XR; off[1] = F16_CC; off[5] = F16_RING; off[6] = F16_SCRATCH;
         off[3] = F16_LASTPROC; off[4] = F16_LASTCHG; off[2] = F16_ORDER;
-        off[0] = F16_ORDER + mceik_align16((size_t)L.ntiles * 2);
+        off[9] = F16_ORDER + mceik_align16((size_t)L.ntiles * 2);
+        off[10] = off[9] + mceik_align16((size_t)L.ntiles);
+        off[0] = off[10] + f16_bitmap_bytes(L);
         return off[0] + nbox;
     }
     const Fsm16Geo g = fsm16_geo(L);
@@ -258,7 +269,9 @@ static inline __host__ __device__ size_t fsm16_smem_layout(const FsmLaunch &L, s
     off[2] = o; o += mceik_align16((size_t)L.ntiles * 2);
     off[3] = o; o += mceik_align16(nb * 2);
     off[4] = o; o += mceik_align16(nb * 2);
-    off[5] = o; o += mceik_align16(nr * 12);
+    off[9] = o; o += mceik_align16((size_t)L.ntiles);
+    off[10] = o; o += f16_bitmap_bytes(L);
+    off[5] = o; o += mceik_align16(nr * 16);
     off[6] = o; o += MCEIK_SCRATCH_BYTES;
     off[7] = o; o += 2 * 4 * MCEIK_X16Q * 4;
     off[8] = o; o += nr * 64 * 4;

@@ -184,7 +184,13 @@ struct BcBoxes {
 
 // Traffic accounting (MCEIK_TRAFFIC builds): lane 0 adds bytes x (lanes where
 // pred holds) to the wave's LDS counter of category k.
-#ifdef MCEIK_TRAFFIC
+#if defined(MCEIK_TRAFFIC) && defined(MCEIK_ADMIT_STATS)
+// (the counters hold admission statistics, fsm16_kernel.hip admit_account16)
+#define TRAF(S, k, pred, bytes) do { (void)(pred); } while (0)
+#define TRAFU(S, k, bytes) do { } while (0)
+#define MCEIK_TRAF_FLUSH_ONLY
+#endif
+#if defined(MCEIK_TRAFFIC) && !defined(MCEIK_TRAF_FLUSH_ONLY)
 #define TRAF(S, k, pred, bytes)                                                                         \
     do {                                                                                                \
         const unsigned n_ = (unsigned)__builtin_popcountll(__ballot(pred));                             \
@@ -194,6 +200,8 @@ struct BcBoxes {
     do {                                                                                                \
         if (threadIdx.x == 0) (S).scratch[8 + (k)] += (int)(bytes);                                     \
     } while (0)
+#endif
+#ifdef MCEIK_TRAFFIC
 // flush the wave's counters to the launch totals (after every sweep / solve)
 #define TRAF_FLUSH(L, S)                                                                                \
     do {                                                                                                \
