@@ -26,6 +26,7 @@
 
 #include "fsm_common.h"
 #include "fsm_device.h"
+#include "fsm_hold.h"
 #include "fsm_update.h"
 #include "mcmc_device.h"
 
@@ -47,7 +48,7 @@ struct Smem16 {
     unsigned short *lastchg;     //   ... of the last visit that changed it
     int *ring_e, *ring_b;        // per position (mod nr): entry tx | ty << 12 | tz << 24 (bubble -1), block id
     unsigned *ring_base;         //   ... byte offset of the tile's line groups
-    unsigned *fmask;             //   ... held stream: what the visit changed (H16_OWN | face bits) | H16_CONT
+    unsigned *fmask;             //   ... held stream: what the visit changed (fsm_hold.h)
     int *scratch;                // visit statistics / traffic counters
     float *xr;                   // neighbour rows XR [4][80][4], then XN (same shape)
     unsigned *meta;              // [nr][64] column meta (flags | tz << 9 | cell-cache base << 16)
@@ -139,14 +140,9 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 #define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
 #endif
 #ifndef MCEIK16_HOLD
-#define MCEIK16_HOLD 1           // the held stream (decide16h): face-level change marks, blocks with an
+#define MCEIK16_HOLD 1           // the held stream (fsm_hold.h): face-level change marks, blocks with an
                                  // in-flight dependency and no settled reason wait instead of being visited
 #endif
-// held stream: the per-position change mask (Smem16.fmask), bit 0 the block changed, bits 1-6 the face
-// layer it changed (x-low, x-high, y-low, y-high, z-low, z-high; absolute orientation), and H16_CONT:
-// the next position continues this position's z-run (same tile, next block in sweep z order)
-#define H16_OWN 1u
-#define H16_CONT 256u
 // BInfo16.w1 bit 24: the brick is the last of its position below the column end, so its z-downwind
 // node is loaded from HBM (into the z-boundary register with the run-start node) for a run that
 // does not continue
@@ -629,176 +625,13 @@ __device__ __forceinline__ int decide16(const FsmLaunch &L, const Fsm16Geo &g, c
     return e;
 }
 
-// ---- the held stream (MCEIK16_HOLD) ------------------------
-// The z-blocks of a sweep are decided tile by tile in diagonal order, but a
-// tile's blocks one at a time (frontier fz, sweep z order), and a block only
-// once the blocks it reads new values from are decided: its sweep-upwind x and
-// y neighbours (the upwind tiles' frontiers are past it) and its z-below (the
-// frontier).  Then, with clocks relative to the sweep:
-//   need >= lastproc (it changed at its last visit, or a neighbour changed
-//     the face layer it shares with it since: settled marks)  -> visit, once
-//     its upwind visits are >= vis positions back (a z-below visited at the
-//     previous position continues the run in registers);
-//   else an upwind neighbour or the z-below still in flight   -> wait (held);
-//   else                                                      -> skip.
-// A skipped block would recompute every node from unchanged inputs, so
-// skipping is exact, like the block-level rule of decide16 (whose in-flight
-// and run-continuation visits almost never change anything: profiles/r05_admit).
-// A visit's changes are "settled" infl positions after it (every lane is past
-// it): the change mask its lanes collected (Smem16.fmask) then marks need of
-// the block itself and of the neighbours across the faces it changed.
-enum { H16_DONE = 0, H16_BLOCKED, H16_HELD, H16_WAIT, H16_SKIP, H16_READY };
-__device__ __forceinline__ int tile_id16(const FsmLaunch &L, const Smem16 &S, int ti, int rx, int ry)
+// the held stream's LDS arrays (fsm_hold.h)
+__device__ __forceinline__ HoldLds<unsigned short> hold_lds16(const Smem16 &S)
 {
-    const int o = S.order[ti];
-    const int txs = o & 0xff, tys = o >> 8;
-    return (ry ? L.nty - 1 - tys : tys) * L.ntx + (rx ? L.ntx - 1 - txs : txs);
-}
-template <bool RZ>
-__device__ __forceinline__ int tile_status16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, int ti, int C,
-                                             int rx, int ry, int &id, int &k, int &runon)
-{
-    const int o = S.order[ti];
-    const int txs = o & 0xff, tys = o >> 8;
-    const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
-    const int nt = L.ntiles, nzk = L.nzk;
-    id = ty * L.ntx + tx;
-    k = S.fz[id];
-    runon = 0;
-    if (k >= nzk) return H16_DONE;
-    const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
-    const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -1;
-    if ((xu >= 0 && (int)S.fz[xu] <= k) || (yu >= 0 && (int)S.fz[yu] <= k)) return H16_BLOCKED;
-    const int tz = RZ ? nzk - 1 - k : k;
-    const int b = tz * nt + id;
-    const bool reason = S.lastchg[b] >= S.lastproc[b];
-    int dep = -0x40000000;                               // latest upwind visit (this sweep's clocks)
-    if (xu >= 0) dep = max(dep, (int)S.lastproc[tz * nt + xu]);
-    if (yu >= 0) dep = max(dep, (int)S.lastproc[tz * nt + yu]);
-    const int zl = k > 0 ? (int)S.lastproc[b + (RZ ? nt : -nt)] : -0x40000000;
-    runon = zl == C - 1;
-    if (!runon) dep = max(dep, zl);
-    if (reason) return dep + g.vis <= C ? H16_READY : H16_WAIT;
-    return (runon || dep > C - g.infl) ? H16_HELD : H16_SKIP;
-}
-// The block of position C (the previous position's ring slot rprev): the next
-// block of the previous position's tile when it is ready, else the first ready
-// block in diagonal order -- windows of 64 tiles from the first incomplete one,
-// every lane deciding its tile's next block per round, until a block is ready
-// or no lane can skip.  Returns the entry tx | ty << 12 | tz << 24, -1 (a
-// bubble) or -2 (every tile decided: the sweep's stream ends).  Progress: the
-// first incomplete tile's upwind tiles are complete, so within infl positions
-// its next block is ready or skipped.
-struct HoldStream {
-    int done;                    // tiles [0, done) of the diagonal order are complete
-    int last;                    // diagonal index of the previous position's tile, -1 none
-};
-template <bool RZ>
-__device__ __forceinline__ int decide16h(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, HoldStream &st,
-                                         int C, int rx, int ry, int rprev, int &zh)
-{
-    const int lane = threadIdx.x, nt = L.ntiles;
-    zh = 0;
-    int pick = -1, pid = 0, pk = 0, pro = 0;
-    if (st.last >= 0) {
-        int id, k, ro;
-        const int s = tile_status16<RZ>(L, g, S, st.last, C, rx, ry, id, k, ro);
-        if (__builtin_amdgcn_readfirstlane(s) == H16_READY) {
-            pick = st.last;
-            pid = __builtin_amdgcn_readfirstlane(id);
-            pk = __builtin_amdgcn_readfirstlane(k);
-            pro = __builtin_amdgcn_readfirstlane(ro);
-        }
-    }
-    if (pick < 0) {
-        for (;;) {                                   // the complete tiles at the front
-            const int ti = st.done + lane;
-            const bool cpl = ti < nt && (int)S.fz[tile_id16(L, S, ti, rx, ry)] >= L.nzk;
-            const unsigned long long m = ~__ballot(cpl);
-            const int n = m ? __builtin_ctzll(m) : 64;
-            st.done += n;
-            if (n < 64) break;
-        }
-        if (st.done >= nt) {
-            st.last = -1;
-            return -2;
-        }
-        for (int base = st.done; base < nt && pick < 0; base += 64) {
-            const int ti = base + lane;
-            for (;;) {
-                int s = H16_DONE, id = 0, k = 0, ro = 0;
-                if (ti < nt) s = tile_status16<RZ>(L, g, S, ti, C, rx, ry, id, k, ro);
-                const bool sk = s == H16_SKIP;
-                if (sk) S.fz[id] = (unsigned char)(k + 1);
-                const unsigned long long rm = __ballot(s == H16_READY);
-                if (rm) {
-                    const int f = __builtin_ctzll(rm);
-                    pick = base + f;
-                    pid = __builtin_amdgcn_readfirstlane(__shfl(id, f, 64));
-                    pk = __builtin_amdgcn_readfirstlane(__shfl(k, f, 64));
-                    pro = __builtin_amdgcn_readfirstlane(__shfl(ro, f, 64));
-                    break;
-                }
-                if (!__ballot(sk)) break;
-                asm volatile("" ::: "memory");       // this round's frontiers feed the next
-            }
-        }
-    }
-    if (pick < 0) {
-        st.last = -1;
-        return -1;
-    }
-    asm volatile("" ::: "memory");
-    if (lane == 0) {
-        S.fz[pid] = (unsigned char)(pk + 1);
-        if (pro) atomicOr(&S.fmask[rprev], H16_CONT);   // the previous position's run continues here
-    }
-    asm volatile("" ::: "memory");
-    st.last = pick;
-    zh = pk > 0 && !pro;                             // a run start above the column's first block
-    const int ty = pid / L.ntx, tx = pid - ty * L.ntx;
-    return tx | (ty << 12) | ((RZ ? L.nzk - 1 - pk : pk) << 24);
-}
-// Settle the visit of ring slot ri (clock clk): its change mask marks need of
-// the block (and the iteration's changed bitmap) and of the neighbours across
-// the changed faces; lanes 0-6 take one target each.
-__device__ __forceinline__ void settle16h(const FsmLaunch &L, const Smem16 &S, int ri, int clk)
-{
-    const int lane = threadIdx.x;
-    asm volatile("" ::: "memory");
-    const int e = S.ring_e[ri];
-    const unsigned m = S.fmask[ri];
-    if (e >= 0 && lane < 7 && ((m >> lane) & 1u)) {
-        const int tx = e & 0xfff, ty = (e >> 12) & 0xfff, tz = (e >> 24) & 0xff;
-        const int nt = L.ntiles, b = tz * nt + ty * L.ntx + tx;
-        const int t = lane == 0 ? b
-                    : lane == 1 ? (tx > 0 ? b - 1 : -1)
-                    : lane == 2 ? (tx < L.ntx - 1 ? b + 1 : -1)
-                    : lane == 3 ? (ty > 0 ? b - L.ntx : -1)
-                    : lane == 4 ? (ty < L.nty - 1 ? b + L.ntx : -1)
-                    : lane == 5 ? (tz > 0 ? b - nt : -1)
-                    : (tz < L.nzk - 1 ? b + nt : -1);
-        if (t >= 0) S.lastchg[t] = (unsigned short)clk;
-        if (lane == 0) S.cbits[b >> 5] |= 1u << (b & 31);
-    }
-    asm volatile("" ::: "memory");
-    if (lane == 0) S.fmask[ri] = 0;
-    asm volatile("" ::: "memory");
-}
-// Start of a held sweep: every block's pending state (need >= lastproc)
-// becomes need 1 / 0 against lastproc 1, the frontiers restart, and the
-// sweep's clock starts at 64 (a sweep needs at most nblocks (1 + infl) + 64
-// < 2^16 clocks: between two visits at most infl bubbles).
-__device__ __forceinline__ void norm16h(const FsmLaunch &L, const Smem16 &S)
-{
-    asm volatile("" ::: "memory");
-    for (int b = threadIdx.x; b < L.nblocks; b += 64) {
-        const bool pend = S.lastchg[b] >= S.lastproc[b];
-        S.lastproc[b] = 1;
-        S.lastchg[b] = pend ? 1 : 0;
-    }
-    for (int t = threadIdx.x; t < L.ntiles; t += 64) S.fz[t] = 0;
-    asm volatile("" ::: "memory");
+    HoldLds<unsigned short> H;
+    H.order = S.order; H.fz = S.fz; H.lastproc = S.lastproc; H.need = S.lastchg; H.fmask = S.fmask;
+    H.ring_e = S.ring_e; H.vbits = S.vbits; H.cbits = S.cbits;
+    return H;
 }
 
 #ifdef MCEIK_ADMIT_STATS
@@ -1073,23 +906,24 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     constexpr bool HOLD = MCEIK16_HOLD;
     HoldStream hs_;
     hs_.done = 0; hs_.last = -1;
+    const HoldLds<unsigned short> H = hold_lds16(S);
     int nset = 0;                                    // held stream: positions settled so far
     // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
     // lane's column is a tile edge (absolute orientation)
-    const unsigned xyface = H16_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
+    const unsigned xyface = HOLD_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
                             (ly == 7 ? 16u : 0u);
     if (HOLD) {
-        norm16h(L, S);
+        hold_norm(L, H);
         clock0 = 64;
     }
     // the next position's block (held stream: after settling the visit infl positions back)
     auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
         if (!HOLD) return decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
         while (nset <= pos - g.infl) {
-            settle16h(L, S, nset % nr, clock0 + nset);
+            hold_settle(L, H, nset % nr, clock0 + nset);
             nset++;
         }
-        return decide16h<RZ>(L, g, S, hs_, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, zh);
+        return hold_decide<RZ>(L, H, hs_, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, g.infl, g.vis, zh);
     };
     constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
     constexpr bool LEAN = KB16 == 2 && MCEIK16_LEAN;     // lean position words (2-step positions)
@@ -1337,7 +1171,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             // the position's last brick: its z-downwind node is the next brick's first (XN row) only
             // when the run continues, else the node loaded from HBM
             fmk = S.fmask[b0.ri()];
-            if ((b0.w1 & W1_ZD) && !(fmk & H16_CONT)) znext = zc;
+            if ((b0.w1 & W1_ZD) && !(fmk & HOLD_CONT)) znext = zc;
         }
         const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
         bool changed = false, nc = false, c0 = false, c15 = false;
@@ -1426,7 +1260,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             // block's lowest / highest node of the column)
             if (changed) {
                 const int zr = LEAN ? (b0.zb() ^ (RZ ? 1 : 0)) : b0.zb() % kb;   // brick index in the block
-                const unsigned m = xyface | ((zr == 0 && c0) ? 32u : 0u) | ((zr == kb - 1 && c15) ? 64u : 0u);
+                const unsigned m = xyface | ((zr == 0 && c0) ? HOLD_ZLO : 0u) | ((zr == kb - 1 && c15) ? HOLD_ZHI : 0u);
                 atomicOr(&S.fmask[b0.ri()], m);
             }
         } else if (changed) {
@@ -1462,7 +1296,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     if (HOLD) {
         // the last visits' changes (every lane is past them)
-        for (; nset < nstream; nset++) settle16h(L, S, nset % nr, clock0 + nset);
+        for (; nset < nstream; nset++) hold_settle(L, H, nset % nr, clock0 + nset);
     }
 #if defined(MCEIK_ADMIT_STATS) && !MCEIK16_HOLD
     admit_flush16(S, nr);
@@ -1716,10 +1550,11 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         // (lastproc 2 > lastchg 1) except the blocks holding boundary-condition
         // nodes (lastchg 3): a block whose nodes and neighbours are all u_nan
         // updates to u_nan, so it needs no visit until a neighbour changes.
-        for (int t = lane; t < L.nblocks; t += 64) {
-            S.lastproc[t] = 2; S.lastchg[t] = 1;
+        if (!MCEIK16_HOLD) {
+            for (int t = lane; t < L.nblocks; t += 64) {
+                S.lastproc[t] = 2; S.lastchg[t] = 1;
+            }
         }
-        if (MCEIK16_HOLD && lane < g.nr) S.fmask[lane] = 0;
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
 #ifdef MCEIK_TRAFFIC
         if (lane == 0)
@@ -1732,25 +1567,15 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<float, 1>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
-        if (lane == 0) {
+        if (MCEIK16_HOLD) {
+            hold_solve_start(L, hold_lds16(S), bc, g.nr);
+        } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
                 for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
                     for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
-                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++) {
-                            const int b = (tz * L.nty + ty) * L.ntx + tx;
-                            S.lastchg[b] = 3;
-                            if (MCEIK16_HOLD) {
-                                // (the held stream marks neighbours only through need: every face
-                                // of a boundary-condition block counts as changed)
-                                if (tx > 0) S.lastchg[b - 1] = 3;
-                                if (tx < L.ntx - 1) S.lastchg[b + 1] = 3;
-                                if (ty > 0) S.lastchg[b - L.ntx] = 3;
-                                if (ty < L.nty - 1) S.lastchg[b + L.ntx] = 3;
-                                if (tz > 0) S.lastchg[b - L.ntiles] = 3;
-                                if (tz < L.nzk - 1) S.lastchg[b + L.ntiles] = 3;
-                            }
-                        }
+                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
+                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = 3;
             }
         }
         asm volatile("" ::: "memory");
@@ -1760,9 +1585,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
                 if (MCEIK16_HOLD) {
-                    // (the held stream rebases its clocks every sweep, norm16h)
-                    for (int w = lane; w < (L.nblocks + 31) / 32; w += 64) { S.vbits[w] = 0; S.cbits[w] = 0; }
-                    asm volatile("" ::: "memory");
+                    hold_iter_start(L, hold_lds16(S));     // (the held stream rebases its clocks every sweep)
                 } else {
                     iter_norm(L, S);
                 }

@@ -123,7 +123,8 @@ static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b
 #ifndef MCEIK_VERIFY_EARLY_EXIT
 #define MCEIK_VERIFY_EARLY_EXIT 1  // convergence verify stops at the first failing node (0: full scan, A/B)
 #endif
-#define MCEIK_SMEM_ARRAYS 12
+#define MCEIK_SMEM_ARRAYS 14      // (+ 12 tile frontier u8 [ntiles], 13 two block bitmaps: the held stream of
+                                  //  the compact layout, fsm_hold.h)
 #define MCEIK_XROWS 80           // neighbour-row array: 64 lanes + 8 x-halo + 8 y-halo rows
 static inline __host__ __device__ size_t mceik_align16(size_t v) { return (v + 15) & ~(size_t)15; }
 // The compile-time-kb cell-cache kernel (fsm_kernel.hip variant 8, the C3
@@ -163,6 +164,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
         off[6] = FSMF_RING; off[7] = FSMF_SCRATCH; off[3] = FSMF_LASTPROC; off[4] = FSMF_LASTCHG;
         off[5] = FSMF_ORDER; off[2] = FSMF_ORDER; off[8] = FSMF_ORDER;          // sf: unused (cells cached)
         off[0] = FSMF_ORDER + mceik_align16((size_t)L.ntiles * 4);
+        off[12] = off[13] = off[0];                                       // (no held stream)
         return off[0] + mceik_align16((size_t)(L.nsrc > 0 ? L.nsrc : 1) * 6 * 4);
     }
     const bool cached = L.slow_mode != 0 && L.cell_cache;
@@ -175,7 +177,9 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[3] = o; o += mceik_align16(nb * (cmp ? 2 : 4));
     off[4] = o; o += mceik_align16(nb * (cmp ? 2 : 4));
     off[5] = o;
-    off[6] = o; o += mceik_align16(nr * (cmp ? 12 : 8));
+    off[6] = o; o += mceik_align16(nr * (cmp ? 16 : 8));       // (cmp: + the held stream's change masks)
+    off[12] = o; o += cmp ? mceik_align16(nt) : 0;
+    off[13] = o; o += cmp ? mceik_align16((nb + 31) / 32 * 4 * 2) : 0;
     off[7] = o; o += MCEIK_SCRATCH_BYTES;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 2 * MCEIK_XROWS * 4 * es;

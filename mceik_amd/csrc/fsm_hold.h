@@ -1,0 +1,271 @@
+// fsm_hold.h -- the held z-block stream of the batched sweep kernels
+// (fsm16_kernel.hip, and fsm_kernel.hip's compact-layout fp64 instances;
+// DESIGN.md s.3.8).
+//
+// EVAL_UPDATE3D (fsm3d.f90:419-456) sweeps every node of the grid in every
+// direction.  The kernels visit only the z-blocks (8x8 column tile x kb
+// bricks) whose inputs changed; skipping the others is exact because a node's
+// update is a pure function of itself, its six neighbours and its slowness,
+// and only lowers it.  The held stream decides which blocks those are:
+//
+// The z-blocks of a sweep are decided tile by tile in diagonal order, but a
+// tile's blocks one at a time (frontier fz, sweep z order), and a block only
+// once the blocks it reads new values from are decided: its sweep-upwind x and
+// y neighbours (the upwind tiles' frontiers are past it) and its z-below (the
+// frontier).  Then, with 16-bit clocks relative to the sweep:
+//   need >= lastproc (it changed at its last visit, or a neighbour changed
+//     the face layer it shares with it since: settled marks)  -> visit, once
+//     its upwind visits are >= vis positions back (a z-below visited at the
+//     previous position continues the run in registers);
+//   else an upwind neighbour or the z-below still in flight   -> wait (held);
+//   else                                                      -> skip.
+// The earlier stream visited every block whose upwind neighbour was still in
+// flight and ran every tile to its column end; those visits almost never
+// changed anything (profiles/r05_admit/bench_admit_stats.log).
+// A visit's changes are "settled" infl positions after it (every lane is past
+// it): the change mask its lanes collected (fmask) then marks need of the
+// block itself and of the neighbours across the faces it changed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fsm_common.h"
+#include "fsm_device.h"
+
+// the per-position change mask (fmask): bit 0 the block changed, bits 1-6 the
+// face layer it changed (x-low, x-high, y-low, y-high, z-low, z-high; absolute
+// orientation), and HOLD_CONT: the next position continues this position's
+// z-run (same tile, next block in sweep z order)
+#define HOLD_OWN 1u
+#define HOLD_ZLO 32u
+#define HOLD_ZHI 64u
+#define HOLD_CONT 256u
+
+namespace {
+
+// The stream's LDS arrays (OrderT: u16 order entries txs | tys << 8, or int
+// entries txs | tys << 16)
+template <typename OrderT>
+struct HoldLds {
+    const OrderT *order;         // diagonal tile order of the (+x, +y) sweep
+    unsigned char *fz;           // per tile: z-blocks decided in this sweep (sweep z order)
+    unsigned short *lastproc;    // per block: clock of its last visit (sweep-relative)
+    unsigned short *need;        // per block: clock of the last settled change of it or of a shared face
+    unsigned *fmask;             // per ring slot: what the position's visit changed | HOLD_CONT
+    const int *ring_e;           // per ring slot: entry tx | ty << 12 | tz << 24, bubble -1
+    unsigned *vbits, *cbits;     // blocks visited / changed in this iteration (bitmaps)
+};
+struct HoldStream {
+    int done;                    // tiles [0, done) of the diagonal order are complete
+    int last;                    // diagonal index of the previous position's tile, -1 none
+};
+enum { HOLD_DONE = 0, HOLD_BLOCKED, HOLD_HELD, HOLD_WAIT, HOLD_SKIP, HOLD_READY };
+
+template <typename OrderT>
+__device__ __forceinline__ void hold_txy(const HoldLds<OrderT> &H, int ti, int &txs, int &tys)
+{
+    constexpr int SH = 4 * (int)sizeof(OrderT);
+    const int o = (int)H.order[ti];
+    txs = o & ((1 << SH) - 1);
+    tys = o >> SH;
+}
+template <typename OrderT>
+__device__ __forceinline__ int hold_tile_id(const FsmLaunch &L, const HoldLds<OrderT> &H, int ti, int rx, int ry)
+{
+    int txs, tys;
+    hold_txy(H, ti, txs, tys);
+    return (ry ? L.nty - 1 - tys : tys) * L.ntx + (rx ? L.ntx - 1 - txs : txs);
+}
+// The next undecided block of the tile at diagonal index ti at clock C:
+// HOLD_DONE / BLOCKED (an upwind tile has not decided that far) / HELD / WAIT
+// (a reason, but an upwind visit is < vis back) / SKIP / READY; id, k: the
+// tile and the block's sweep-z index, runon: its z-below is the previous position.
+template <bool RZ, typename OrderT>
+__device__ __forceinline__ int hold_status(const FsmLaunch &L, const HoldLds<OrderT> &H, int ti, int C, int rx, int ry,
+                                           int infl, int vis, int &id, int &k, int &runon)
+{
+    int txs, tys;
+    hold_txy(H, ti, txs, tys);
+    const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+    const int nt = L.ntiles, nzk = L.nzk;
+    id = ty * L.ntx + tx;
+    k = H.fz[id];
+    runon = 0;
+    if (k >= nzk) return HOLD_DONE;
+    const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
+    const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -1;
+    if ((xu >= 0 && (int)H.fz[xu] <= k) || (yu >= 0 && (int)H.fz[yu] <= k)) return HOLD_BLOCKED;
+    const int tz = RZ ? nzk - 1 - k : k;
+    const int b = tz * nt + id;
+    const bool reason = H.need[b] >= H.lastproc[b];
+    int dep = -0x40000000;                               // latest upwind visit (this sweep's clocks)
+    if (xu >= 0) dep = max(dep, (int)H.lastproc[tz * nt + xu]);
+    if (yu >= 0) dep = max(dep, (int)H.lastproc[tz * nt + yu]);
+    const int zl = k > 0 ? (int)H.lastproc[b + (RZ ? nt : -nt)] : -0x40000000;
+    runon = zl == C - 1;
+    if (!runon) dep = max(dep, zl);
+    if (reason) return dep + vis <= C ? HOLD_READY : HOLD_WAIT;
+    return (runon || dep > C - infl) ? HOLD_HELD : HOLD_SKIP;
+}
+// The block of position C (the previous position's ring slot rprev): the next
+// block of the previous position's tile when it is ready, else the first ready
+// block in diagonal order -- windows of 64 tiles from the first incomplete one,
+// every lane deciding its tile's next block per round, until a block is ready
+// or no lane can skip.  Returns the entry tx | ty << 12 | tz << 24, -1 (a
+// bubble) or -2 (every tile decided: the sweep's stream ends); zh: a run start
+// above the column's first block (its z-upwind node comes from HBM).
+// Progress: the first incomplete tile's upwind tiles are complete, so within
+// infl positions its next block is ready or skipped.
+template <bool RZ, typename OrderT>
+__device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<OrderT> &H, HoldStream &st, int C, int rx,
+                                           int ry, int rprev, int infl, int vis, int &zh)
+{
+    const int lane = threadIdx.x, nt = L.ntiles;
+    zh = 0;
+    int pick = -1, pid = 0, pk = 0, pro = 0;
+    if (st.last >= 0) {
+        int id, k, ro;
+        const int s = hold_status<RZ>(L, H, st.last, C, rx, ry, infl, vis, id, k, ro);
+        if (__builtin_amdgcn_readfirstlane(s) == HOLD_READY) {
+            pick = st.last;
+            pid = __builtin_amdgcn_readfirstlane(id);
+            pk = __builtin_amdgcn_readfirstlane(k);
+            pro = __builtin_amdgcn_readfirstlane(ro);
+        }
+    }
+    if (pick < 0) {
+        for (;;) {                                   // the complete tiles at the front
+            const int ti = st.done + lane;
+            const bool cpl = ti < nt && (int)H.fz[hold_tile_id(L, H, ti, rx, ry)] >= L.nzk;
+            const unsigned long long m = ~__ballot(cpl);
+            const int n = m ? __builtin_ctzll(m) : 64;
+            st.done += n;
+            if (n < 64) break;
+        }
+        if (st.done >= nt) {
+            st.last = -1;
+            return -2;
+        }
+        for (int base = st.done; base < nt && pick < 0; base += 64) {
+            const int ti = base + lane;
+            for (;;) {
+                int s = HOLD_DONE, id = 0, k = 0, ro = 0;
+                if (ti < nt) s = hold_status<RZ>(L, H, ti, C, rx, ry, infl, vis, id, k, ro);
+                const bool sk = s == HOLD_SKIP;
+                if (sk) H.fz[id] = (unsigned char)(k + 1);
+                const unsigned long long rm = __ballot(s == HOLD_READY);
+                if (rm) {
+                    const int f = __builtin_ctzll(rm);
+                    pick = base + f;
+                    pid = __builtin_amdgcn_readfirstlane(__shfl(id, f, 64));
+                    pk = __builtin_amdgcn_readfirstlane(__shfl(k, f, 64));
+                    pro = __builtin_amdgcn_readfirstlane(__shfl(ro, f, 64));
+                    break;
+                }
+                if (!__ballot(sk)) break;
+                asm volatile("" ::: "memory");       // this round's frontiers feed the next
+            }
+        }
+    }
+    if (pick < 0) {
+        st.last = -1;
+        return -1;
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0) {
+        H.fz[pid] = (unsigned char)(pk + 1);
+        if (pro) atomicOr(&H.fmask[rprev], HOLD_CONT);   // the previous position's run continues here
+    }
+    asm volatile("" ::: "memory");
+    st.last = pick;
+    zh = pk > 0 && !pro;
+    const int ty = pid / L.ntx, tx = pid - ty * L.ntx;
+    return tx | (ty << 12) | ((RZ ? L.nzk - 1 - pk : pk) << 24);
+}
+// Settle the visit of ring slot ri (clock clk): its change mask marks need of
+// the block (and the iteration's changed bitmap) and of the neighbours across
+// the changed faces; lanes 0-6 take one target each.
+template <typename OrderT>
+__device__ __forceinline__ void hold_settle(const FsmLaunch &L, const HoldLds<OrderT> &H, int ri, int clk)
+{
+    const int lane = threadIdx.x;
+    asm volatile("" ::: "memory");
+    const int e = H.ring_e[ri];
+    const unsigned m = H.fmask[ri];
+    if (e >= 0 && lane < 7 && ((m >> lane) & 1u)) {
+        const int tx = e & 0xfff, ty = (e >> 12) & 0xfff, tz = (e >> 24) & 0xff;
+        const int nt = L.ntiles, b = tz * nt + ty * L.ntx + tx;
+        const int t = lane == 0 ? b
+                    : lane == 1 ? (tx > 0 ? b - 1 : -1)
+                    : lane == 2 ? (tx < L.ntx - 1 ? b + 1 : -1)
+                    : lane == 3 ? (ty > 0 ? b - L.ntx : -1)
+                    : lane == 4 ? (ty < L.nty - 1 ? b + L.ntx : -1)
+                    : lane == 5 ? (tz > 0 ? b - nt : -1)
+                    : (tz < L.nzk - 1 ? b + nt : -1);
+        if (t >= 0) H.need[t] = (unsigned short)clk;
+        if (lane == 0) H.cbits[b >> 5] |= 1u << (b & 31);
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0) H.fmask[ri] = 0;
+    asm volatile("" ::: "memory");
+}
+// Start of a sweep: every block's pending state (need >= lastproc) becomes
+// need 1 / 0 against lastproc 1, the frontiers restart, and the sweep's clock
+// starts at 64 (a sweep needs at most nblocks (1 + infl) + 64 < 2^16 clocks:
+// between two visits at most infl bubbles).
+template <typename OrderT>
+__device__ __forceinline__ void hold_norm(const FsmLaunch &L, const HoldLds<OrderT> &H)
+{
+    asm volatile("" ::: "memory");
+    for (int b = threadIdx.x; b < L.nblocks; b += 64) {
+        const bool pend = H.need[b] >= H.lastproc[b];
+        H.lastproc[b] = 1;
+        H.need[b] = pend ? 1 : 0;
+    }
+    for (int t = threadIdx.x; t < L.ntiles; t += 64) H.fz[t] = 0;
+    asm volatile("" ::: "memory");
+}
+// Start of an iteration: no block visited or changed yet.
+template <typename OrderT>
+__device__ __forceinline__ void hold_iter_start(const FsmLaunch &L, const HoldLds<OrderT> &H)
+{
+    for (int w = threadIdx.x; w < (L.nblocks + 31) / 32; w += 64) {
+        H.vbits[w] = 0;
+        H.cbits[w] = 0;
+    }
+    asm volatile("" ::: "memory");
+}
+// Start of a solve (before the first sweep): every block visited at 2 and
+// not pending (need 1), except the blocks holding boundary-condition nodes
+// and their face neighbours (need 3): a block whose nodes and neighbours are
+// all u_nan updates to u_nan.  Lane 0 marks the boxes' blocks.
+template <typename OrderT>
+__device__ __forceinline__ void hold_solve_start(const FsmLaunch &L, const HoldLds<OrderT> &H, const BcBoxes &bc, int nr)
+{
+    const int lane = threadIdx.x;
+    for (int t = lane; t < L.nblocks; t += 64) {
+        H.lastproc[t] = 2;
+        H.need[t] = 1;
+    }
+    if (lane < nr) H.fmask[lane] = 0;
+    asm volatile("" ::: "memory");
+    if (lane == 0) {
+        for (int k = 0; k < bc.n; k++) {
+            const int *q = bc.box + 6 * k;
+            for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
+                for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
+                    for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++) {
+                        const int b = (tz * L.nty + ty) * L.ntx + tx;
+                        H.need[b] = 3;
+                        if (tx > 0) H.need[b - 1] = 3;
+                        if (tx < L.ntx - 1) H.need[b + 1] = 3;
+                        if (ty > 0) H.need[b - L.ntx] = 3;
+                        if (ty < L.nty - 1) H.need[b + L.ntx] = 3;
+                        if (tz > 0) H.need[b - L.ntiles] = 3;
+                        if (tz < L.nzk - 1) H.need[b + L.ntiles] = 3;
+                    }
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+
+}  // namespace

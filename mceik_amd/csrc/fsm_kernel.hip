@@ -23,7 +23,13 @@
 
 #include "fsm_common.h"
 #include "fsm_device.h"
+#include "fsm_hold.h"
 #include "fsm_update.h"
+
+// the held z-block stream (fsm_hold.h) for the compact-layout fp64 instances
+#ifndef MCEIK8_HOLD
+#define MCEIK8_HOLD 1
+#endif
 
 namespace {
 
@@ -62,6 +68,9 @@ struct Smem {
     unsigned *meta;              // CMP: [nr][64] the meta word only (own column = tile base + lane column)
     R *sf;                       // staged slowness*h (modes 0,1)
     R *xr;                       // neighbour rows: XR [2 halves][80 rows][4], then XN (same shape)
+    unsigned *fmask;             // CMP, held stream: per ring slot, what the position's visit changed
+    unsigned char *fz;           // CMP, held stream: per tile, z-blocks decided in this sweep
+    unsigned *vbits, *cbits;     // CMP, held stream: blocks visited / changed in this iteration
 };
 
 template <typename R, bool FIXED, bool CMP>
@@ -87,7 +96,20 @@ __device__ __forceinline__ Smem<R, CMP> smem_bind(const FsmLaunch &L, unsigned c
     S.xr = reinterpret_cast<R *>(base + off[9]);       // arrays 9 (XR) and 10 (XN) are contiguous
     S.cinfo = reinterpret_cast<u2v *>(base + off[11]);
     S.meta = reinterpret_cast<unsigned *>(base + off[11]);
+    S.fmask = reinterpret_cast<unsigned *>(S.ring + 3 * L.nr);
+    S.fz = base + off[12];
+    S.vbits = reinterpret_cast<unsigned *>(base + off[13]);
+    S.cbits = S.vbits + (L.nblocks + 31) / 32;
     return S;
+}
+// the held stream's LDS arrays (compact layout only: 16-bit clocks)
+template <typename R>
+__device__ __forceinline__ HoldLds<int> hold_lds(const Smem<R, true> &S)
+{
+    HoldLds<int> H;
+    H.order = S.order; H.fz = S.fz; H.lastproc = S.lastproc; H.need = S.lastchg; H.fmask = S.fmask;
+    H.ring_e = S.ring; H.vbits = S.vbits; H.cbits = S.cbits;
+    return H;
 }
 // column info {own column, meta} of lane l at ring slot ri (col: lane l's
 // column offset inside its tile, used by the compact layout)
@@ -111,6 +133,8 @@ struct BInfo {
     int bid;                 // z-block id (stamps)
     int clk;                 // stream position of the brick (stamps)
     int bcm;                 // BC z-slots of the segment (generic path)
+    bool zd;                 // held stream: the position's last brick below the column end -- zh is then
+                             // its z-downwind node, the next brick's first only when the run continues
 };
 
 template <typename R, bool RZ, int ZSH, bool CMP>
@@ -136,6 +160,11 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Sm
     if (zb == (RZ ? L.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : L.nzb - 1)) fl |= F_LAST;
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
+    b.zd = CMP && MCEIK8_HOLD && valid && p.zbs == kb - 1 && !(fl & F_LAST);
+    if (b.zd) {
+        const int zn = RZ ? zb * 8 - 1 : zb * 8 + 8;          // z-downwind node of the brick's last slot
+        b.zh = ci.x + zoff_bytes<R>(zn >> 3) + (uint32_t)(zn & 7) * (uint32_t)sizeof(R);
+    }
     bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && b.zb8 + 8 > L.nz);
     b.bcm = 0;
     if (__any(fl & C_BC)) {
@@ -454,7 +483,9 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R, 
         tbase = (uint32_t)((entry & 0xfff) + ((entry >> 12) & 0xfff) * L.ntx) * tile_bytes<R>(L);
         nbv = min(kb, L.nzb - tz * kb);
         // first visit of the block in this iteration: no visit since the iteration's first clock
-        const int u0flag = (int)S.lastproc[bid] < clock_it;
+        // (held stream: its clocks restart every sweep, the iteration's visits are a bitmap)
+        const int u0flag = (CMP && MCEIK8_HOLD) ? !((S.vbits[bid >> 5] >> (bid & 31)) & 1u)
+                                                : (int)S.lastproc[bid] < clock_it;
         if ((entry & 0xffffff) != ct.tile) column_tile<R>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         ci.x = ct.col;
         ci.y = column_word(L, kb, ct, tz, ri, u0flag, zh);
@@ -471,6 +502,7 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R, 
         if (CMP) S.ring[2 * L.nr + ri] = (int)tbase;
         if (entry >= 0) {
             S.lastproc[bid] = (typename Smem<R, CMP>::clk_t)clock;
+            if (CMP && MCEIK8_HOLD) S.vbits[bid >> 5] |= 1u << (bid & 31);
             if (L.visit_stats) {
                 S.scratch[0] += nbv;
                 S.scratch[1] += nbv * nact;
@@ -521,7 +553,8 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R, CMP>
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC, bool CMP>
 __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, CMP> &S, const BInfo &b0, R (&c)[8],
                                              R (&n)[8], R (&r)[8], R zc, int lx, int ly, int rx, int ry,
-                                             bool &changed, bool &nc, int &ierr_last)
+                                             bool &changed, bool &nc, int &ierr_last, bool zdsel, bool &c0,
+                                             bool &c7)
 {
     const int lane = threadIdx.x;
     const R T = (R)L.conv_thresh;
@@ -554,7 +587,8 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
     const int oxp = XROW(1, 0, lxs < 7 ? lane + 1 : 64 + lys), oyp = XROW(1, 0, lys < 7 ? lane + 8 : 72 + lxs);
     // fp64: the next brick's first slot from this lane's XN row (the sweep
     // keeps no register copy of the next brick)
-    const R nfirst = LAZY ? S.xr[XROW(1, RZ ? 1 : 0, lane) + (RZ ? 3 : 0)] : n[RZ ? 7 : 0];
+    R nfirst = LAZY ? S.xr[XROW(1, RZ ? 1 : 0, lane) + (RZ ? 3 : 0)] : n[RZ ? 7 : 0];
+    if (zdsel) nfirst = zc;                  // held stream: a run end below the column end (HBM node)
     if (!LAZY) {
         load_row(S.xr, oxm, xmr);
         load_row(S.xr, oym, ymr);
@@ -614,6 +648,8 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
         const bool dec = nv < self;
         nc |= dec && (self >= T || (MCEIK_BIGSTEP && sizeof(R) == 8 && self - nv >= TB));
         changed |= dec;
+        if (pj == 0) c0 = dec;               // the brick's lowest / highest node changed (z faces of
+        if (pj == 7) c7 = dec;               //   its block, held stream)
         r[pj] = nv;
     }
 }
@@ -648,6 +684,32 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     // stream bookkeeping (wave-uniform)
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
+    // the held stream (compact layout; fsm_hold.h): clocks restart at 64 every sweep
+    constexpr bool HOLD = CMP && MCEIK8_HOLD;
+    HoldStream hs_;
+    hs_.done = 0; hs_.last = -1;
+    int nset = 0;                                    // positions settled so far
+    // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
+    // lane's column is a tile edge (absolute orientation)
+    const unsigned xyface = HOLD_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
+                            (ly == 7 ? 16u : 0u);
+    if constexpr (HOLD) {
+        hold_norm(L, hold_lds(S));
+        clock0 = 64;
+    }
+    // the next position's block (held stream: after settling the visit infl positions back)
+    auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
+        if constexpr (HOLD) {
+            const HoldLds<int> H = hold_lds(S);
+            while (nset <= pos - L.infl) {
+                hold_settle(L, H, nset % nr, clock0 + nset);
+                nset++;
+            }
+            return hold_decide<RZ>(L, H, hs_, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, L.infl, L.vis, zh);
+        } else {
+            return decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
+        }
+    };
     R c[8], n[8], q[8], p[8], r[8], fq[8], hq[4], hn[4];
     constexpr bool PAIR = MCEIK_PAIR_LOAD && sizeof(R) == 4 && MCEIK_AHEAD == 2;
     // FL64: whole-line own loads (line_issue64): la / lh this step's quarters
@@ -669,7 +731,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     constexpr int AH = MCEIK_AHEAD;      // own segments loaded AH steps ahead (2 or 3)
     for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
         int zh;
-        const int e = decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
+        const int e = decide_any(pos, dri, zh);
         if (e == -2) {
             if (pos == 0) return 0;                         // nothing changed near any block: skip the sweep
             nstream = pos;
@@ -797,7 +859,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (ph == 0 && nstream == 0x7fffffff) {
             const int pos = ndecided;
             int zh;
-            const int e = decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
+            const int e = decide_any(pos, dri, zh);
             if (e == -2) {
                 nstream = pos;
             } else {
@@ -852,14 +914,16 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
         if (SLOWMODE != 2) prefetch_slow<R, SLOWMODE>(L, S, sr, b1, lx, ly, fq);
 
-        // ---- the 8 z-slots of the current brick
-        bool changed = false, nc = false;
+        // ---- the 8 z-slots of the current brick (held stream: a run end's z-downwind node is the
+        // one loaded from HBM)
+        bool changed = false, nc = false, c0 = false, c7 = false;
+        const bool zdsel = HOLD && b0.zd && !(S.fmask[b0.ri] & HOLD_CONT);
         if (__any(b0.fl & F_SLOW))
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
-                                                           ierr_last);
+                                                           ierr_last, zdsel, c0, c7);
         else
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, false>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
-                                                            ierr_last);
+                                                            ierr_last, zdsel, c0, c7);
         const bool val = (b0.fl & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
@@ -948,7 +1012,17 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             TRAF(S, 3, changed, 8 * sizeof(R));
         }
         if (!LAZYN) u0_store();
-        if (changed) S.lastchg[b0.bid] = (typename Smem<R, CMP>::clk_t)(clock0 + b0.clk);   // lanes of one block write the same value
+        if constexpr (HOLD) {
+            // what this lane changed: the block, its x / y faces (edge columns), its z faces (the
+            // block's lowest / highest node of the column)
+            if (changed) {
+                const int zr = (b0.zb8 >> 3) % kb;                 // brick index in the block
+                const unsigned m = xyface | ((zr == 0 && c0) ? HOLD_ZLO : 0u) | ((zr == kb - 1 && c7) ? HOLD_ZHI : 0u);
+                atomicOr(&S.fmask[b0.ri], m);
+            }
+        } else if (changed) {
+            S.lastchg[b0.bid] = (typename Smem<R, CMP>::clk_t)(clock0 + b0.clk);   // lanes of one block write the same value
+        }
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < 8; i++) {
@@ -998,6 +1072,11 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         }
     }
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
+    if constexpr (HOLD) {
+        // the last visits' changes (every lane is past them)
+        const HoldLds<int> H = hold_lds(S);
+        for (; nset < nstream; nset++) hold_settle(L, H, nset % nr, clock0 + nset);
+    }
     return nstream;
 }
 
@@ -1047,7 +1126,8 @@ __device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u
     const R T = (R)L.conv_thresh, tolr = (R)L.tol;
     for (int base = 0; base < L.nblocks; base += 64) {
         const int k = base + lane;
-        const bool flag = k < L.nblocks && S.lastchg[k] >= clock_it;
+        const bool flag = k < L.nblocks && ((CMP && MCEIK8_HOLD) ? ((S.cbits[k >> 5] >> (k & 31)) & 1u) != 0
+                                                                 : S.lastchg[k] >= clock_it);
         unsigned long long m = __ballot(flag);
         while (m) {
             const int bid = base + __builtin_ctzll(m);
@@ -1130,8 +1210,11 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         // (compact layout: 16-bit clocks relative to the iteration, the same
         // order -- visited 2, changed 1, BC blocks changed 3 -- rebased by
         // iter_norm at every iteration start, where the clock restarts at 64)
-        for (int t = lane; t < L.nblocks; t += 64) {
-            S.lastproc[t] = CMP ? 2 : -2; S.lastchg[t] = CMP ? 1 : -3;
+        constexpr bool HOLD = CMP && MCEIK8_HOLD;
+        if (!HOLD) {
+            for (int t = lane; t < L.nblocks; t += 64) {
+                S.lastproc[t] = CMP ? 2 : -2; S.lastchg[t] = CMP ? 1 : -3;
+            }
         }
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
 #ifdef MCEIK_TRAFFIC
@@ -1142,7 +1225,9 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
-        if (lane == 0) {
+        if constexpr (HOLD) {
+            hold_solve_start(L, hold_lds(S), bc, L.nr);
+        } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
                 for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
@@ -1157,7 +1242,10 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
-                if (CMP) {
+                if constexpr (HOLD) {
+                    hold_iter_start(L, hold_lds(S));      // (the held stream rebases its clocks every sweep)
+                    clock = 64;
+                } else if (CMP) {
                     iter_norm(L, S);
                     clock = 64;
                 }
