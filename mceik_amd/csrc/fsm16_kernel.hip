@@ -375,11 +375,11 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
     int fl = valid ? (int)((meta & 0x7f) | F_VALID) : 0;
     if (zb == (RZ ? g.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : g.nzb - 1)) fl |= F_LAST;
+    // held stream: the z-boundary nodes come from the z-face copies (zf), the run end's z-downwind
+    // node of the position's last brick below the column end included
     const bool zd = MCEIK16_HOLD && valid && p.zbs == kb - 1 && !(fl & F_LAST);
-    if (zd) {
-        const int zn = RZ ? zb * 16 - 1 : zb * 16 + 16;      // z-downwind node of the brick's last slot
-        b.zh = col + zoff16(zn >> 4) + (uint32_t)(zn & 15) * 4u;
-    }
+    if (MCEIK16_HOLD && b.zh != OOB) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], false, lx, ly);
+    if (zd) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], true, lx, ly);
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
     bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && zb * 16 + 16 > L.nz);
     unsigned bcm = 0;
@@ -463,10 +463,11 @@ __device__ __forceinline__ BInfo16 brick_info_lean(const FsmLaunch &L, const Sme
     b.seg = valid ? off : OOB;
     b.lseg = pv && (w & ((16u << LW_G(0)) | (16u << LW_G(1)))) ? off : OOB;
     b.zh = valid && (gp & 8u) ? off + (RZ ? 8192u - 64u : 124u - 8192u) : OOB;
-    // the last brick of the position below the column end: its z-downwind node (the next line group's
-    // first node, or the previous one's last node when z descends)
+    // held stream: the z-boundary nodes come from the z-face copies (zf), the run end's z-downwind
+    // node of the position's last brick below the column end included
     const bool zd = MCEIK16_HOLD && valid && ph == 1 && !(gp & 2u);
-    if (zd) b.zh = off + (RZ ? 124u - 8192u : 8192u - 64u);
+    if (MCEIK16_HOLD && b.zh != OOB) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], false, lx, ly);
+    if (zd) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], true, lx, ly);
     int fl = valid ? (int)((w & 0x7fu) | F_VALID | ((gp & 15u) << 8)) : 0;
     unsigned bcm = 0;
     if (__any(fl & C_BC)) {
@@ -883,10 +884,11 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
 // 16-z bricks and the brick values updated in place: a lane's next brick
 // lives in its XN row and is read back into v at the end of the step.
 template <bool RZ, int KB16, int CCR>
-__device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr,
+__device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr, Rsrc zfr,
                                        const BcBoxes &bc, const Smem16 &S, int rx, int ry, int clock0, bool &notconv,
                                        int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
+    const Rsrc zr_ = MCEIK16_HOLD ? zfr : ur;        // where the z-boundary nodes are read
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const float UN = FLT_MAX;
@@ -997,7 +999,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hq[4]));
         TRAF(S, 1, ho != OOB, 32);
     }
-    zc = bload1(ur, b0.zh, 0.0f);
+    zc = bload1(zr_, b0.zh, 0.0f);
     TRAF(S, 0, b0.seg != OOB, 64);
     TRAF(S, 2, b0.zh != OOB, 4);
     pos_adv(p3, kb, nr);
@@ -1058,7 +1060,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         bload4h(ur, ho + 16u, *reinterpret_cast<float (*)[4]>(&hn[4]));
         TRAF(S, 1, ho != OOB, 32);
     }
-    zn = bload1(ur, b1.zh, 0.0f);
+    zn = bload1(zr_, b1.zh, 0.0f);
     TRAF(S, 0, b1.seg != OOB, 64);
     TRAF(S, 2, b1.zh != OOB, 4);
     {
@@ -1133,7 +1135,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             line_issue(ur, b3.lseg, p3.vb >= 0 && p3.zbs == 0, lq, hpnew);
         else
             seg_issue(ur, b3.seg, qa);
-        zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, 0.0f) : 0.0f;
+        zq = __any(b3.zh != OOB) ? bload1(zr_, b3.zh, 0.0f) : 0.0f;
         if (HFL) {
             const uint32_t lo = halo_line_lean<RZ>(pe, nstream, me, ce, hbit, hdelta);
             const uint32_t lp = dpp_swap_quad_half(lo);
@@ -1258,10 +1260,13 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         if (HOLD) {
             // what this lane changed: the block, its x / y faces (edge columns), its z faces (the
             // block's lowest / highest node of the column)
-            if (changed) {
-                const int zr = LEAN ? (b0.zb() ^ (RZ ? 1 : 0)) : b0.zb() % kb;   // brick index in the block
-                const unsigned m = xyface | ((zr == 0 && c0) ? HOLD_ZLO : 0u) | ((zr == kb - 1 && c15) ? HOLD_ZHI : 0u);
-                atomicOr(&S.fmask[b0.ri()], m);
+            const int zr = LEAN ? (b0.zb() ^ (RZ ? 1 : 0)) : b0.zb() % kb;   // brick index in the block
+            const bool zlo = changed && zr == 0 && c0, zhi = changed && zr == kb - 1 && c15;
+            if (changed) atomicOr(&S.fmask[b0.ri()], xyface | (zlo ? HOLD_ZLO : 0u) | (zhi ? HOLD_ZHI : 0u));
+            // the block's lowest / highest node of this column changed: its z-face copy too
+            if (__any(zlo || zhi)) {
+                bstore1(zfr, zlo ? zf_off<float>(b0.bid(), 0, lx, ly) : OOB, v[0]);
+                bstore1(zfr, zhi ? zf_off<float>(b0.bid(), 1, lx, ly) : OOB, v[15]);
             }
         } else if (changed) {
             S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
@@ -1546,6 +1551,8 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         const void *slow_model = reinterpret_cast<const float *>(L.slow) + sentry * ncell;
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
                    sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
+        const size_t zfb = MCEIK16_HOLD ? zf_bytes(L, 4) : 0;
+        const Rsrc zfr = make_rsrc(reinterpret_cast<char *>(L.zf) + (size_t)blockIdx.x * zfb, (uint32_t)zfb);
         // Before the first sweep every block counts as visited and unchanged
         // (lastproc 2 > lastchg 1) except the blocks holding boundary-condition
         // nodes (lastchg 3): a block whose nodes and neighbours are all u_nan
@@ -1569,6 +1576,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         const bool ok = init_field<float, 1>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
         if (MCEIK16_HOLD) {
             hold_solve_start(L, hold_lds16(S), bc, g.nr);
+            zf_init<float>(L, zfr, u, bc);
         } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
@@ -1595,10 +1603,10 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
                     // positions used + a gap of infl: the previous sweep's visits are
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
-                        clock += g.infl + sweep16<true, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                        clock += g.infl + sweep16<true, KB16, CCR>(L, g, ur, u0r, sr, zfr, bc, S, rx, ry, clock, notconv,
                                                               ierr_last, nchg, nsteps);
                     else
-                        clock += g.infl + sweep16<false, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                        clock += g.infl + sweep16<false, KB16, CCR>(L, g, ur, u0r, sr, zfr, bc, S, rx, ry, clock, notconv,
                                                                ierr_last, nchg, nsteps);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

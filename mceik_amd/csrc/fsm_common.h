@@ -38,6 +38,9 @@ struct FsmLaunch {
     size_t field_elems;          // ntiles * nzq * 64 * (128 / es)
     void *u;                     // travel-time fields (brick layout, R)
     void *u0;                    // convergence side field (same layout)
+    void *zf;                    // held stream: per-wave copies of every z-block's lowest and highest node per
+                                 // column, [nblocks][2][64 columns lx + 8 ly] R (zf_bytes), the values a run
+                                 // start / end reads across a z-block boundary
     int slot_per_solve;          // 1: field slot = solve id; 0: slot = blockIdx.x (scratch)
     const int *ev_node;          // event nodes (x-fastest linear index), may be null
     int nev;
@@ -88,6 +91,8 @@ static inline __host__ __device__ size_t fsm_slow_entry(const FsmLaunch &L, int 
 }
 
 static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
+// bytes of one wave's z-face copies (FsmLaunch.zf)
+static inline __host__ __device__ size_t zf_bytes(const FsmLaunch &L, size_t es) { return (size_t)L.nblocks * 128 * es; }
 
 // Debug / accounting counters in LDS: [0..3] visit statistics; MCEIK_TRAFFIC
 // builds add [8..15], the requested global-memory bytes of the wave's current

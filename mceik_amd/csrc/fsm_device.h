@@ -248,6 +248,14 @@ __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, double (&v)[4])
     d2v b = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
 }
+__device__ __forceinline__ void bstore1(Rsrc r, uint32_t off, float v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore1(Rsrc r, uint32_t off, double v)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, off, 0, 0);
+}
 __device__ __forceinline__ float bload1(Rsrc r, uint32_t off, float)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));

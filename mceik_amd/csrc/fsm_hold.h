@@ -268,4 +268,59 @@ __device__ __forceinline__ void hold_solve_start(const FsmLaunch &L, const HoldL
     asm volatile("" ::: "memory");
 }
 
+// ---- z-face copies (FsmLaunch.zf) -----------------------------------------
+// A run that starts above a column's first block reads its z-upwind node, and
+// one that ends below the column's last block its z-downwind node, across a
+// z-block boundary.  Read from the field those are one value per 128-B line
+// of 64 columns; the held stream starts and ends runs at about half its
+// positions, so the kernels keep a copy of every block's lowest and highest
+// node per column (zf, [nblocks][2][64] R, columns lx + 8 ly), rewritten with
+// the field whenever such a node changes, and read 64 columns from 256 B.
+// Offset of block b's side (0: lowest node, 1: highest) of column (lx, ly).
+template <typename R>
+__device__ __forceinline__ uint32_t zf_off(int b, int side, int lx, int ly)
+{
+    return ((uint32_t)(b * 2 + side) * 64u + (uint32_t)(lx + 8 * ly)) * (uint32_t)sizeof(R);
+}
+// The z-boundary node a brick of block b reads in sweep direction RZ: the
+// z-upwind node of a run start (the z-below block's facing side), or the
+// z-downwind node of a run end (zd: the z-above block's facing side).
+template <typename R, bool RZ>
+__device__ __forceinline__ uint32_t zf_boundary(const FsmLaunch &L, int b, bool zd, int lx, int ly)
+{
+    // sweep z ascending: below = tz - 1 (its highest node), above = tz + 1 (its lowest)
+    const bool up = zd != RZ;                               // the neighbour is at tz + 1
+    return zf_off<R>(b + (up ? L.ntiles : -L.ntiles), up ? 0 : 1, lx, ly);
+}
+// Start of a solve (after init_field, whose stores have completed): every
+// copy is u_nan except the boundary-condition nodes on a block's lowest or
+// highest layer, copied from the field (lanes 0-26: the 3 x 3 x 3 candidate
+// nodes of each source box).
+template <typename R>
+__device__ __forceinline__ void zf_init(const FsmLaunch &L, Rsrc zfr, const R *u, const BcBoxes &bc)
+{
+    const int lane = threadIdx.x;
+    const R UN = Num<R>::unan();
+    R fill[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) fill[i] = UN;
+    const uint32_t nvec = (uint32_t)(zf_bytes(L, sizeof(R)) / (8 * sizeof(R)));
+    for (uint32_t i = lane; i < nvec; i += 64) bstore8(zfr, i * 8u * (uint32_t)sizeof(R), fill);
+    __builtin_amdgcn_s_waitcnt(0);
+    const int zbk = 8 * L.kb;                                  // z per block
+    for (int s = 0; s < bc.n; s++) {
+        const int *q = bc.box + 6 * s;
+        const int x = q[0] + lane % 3, y = q[2] + (lane / 3) % 3, z = q[4] + lane / 9;
+        if (lane < 27 && x <= q[1] && y <= q[3] && z <= q[5]) {
+            const int zr = z % zbk;
+            if (zr == 0 || zr == zbk - 1) {
+                const int b = ((z / zbk) * L.nty + (y >> 3)) * L.ntx + (x >> 3);
+                bstore1(zfr, zf_off<R>(b, zr == 0 ? 0 : 1, x & 7, y & 7), u[brick_index<R>(L, x, y, z)]);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
 }  // namespace

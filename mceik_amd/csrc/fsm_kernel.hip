@@ -30,6 +30,11 @@
 #ifndef MCEIK8_HOLD
 #define MCEIK8_HOLD 1
 #endif
+// ... with its z-boundary nodes from the z-face copies (FsmLaunch.zf) instead of the field: off, measured
+// 2.4% slower in fp64 (the copies' stores and their buffer descriptor spill registers; profiles/r05_zf)
+#ifndef MCEIK8_ZF
+#define MCEIK8_ZF 0
+#endif
 
 namespace {
 
@@ -160,8 +165,13 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Sm
     if (zb == (RZ ? L.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : L.nzb - 1)) fl |= F_LAST;
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
+    // held stream: the z-boundary nodes come from the z-face copies (zf), the run end's z-downwind
+    // node of the position's last brick below the column end included
     b.zd = CMP && MCEIK8_HOLD && valid && p.zbs == kb - 1 && !(fl & F_LAST);
-    if (b.zd) {
+    if (CMP && MCEIK8_HOLD && MCEIK8_ZF) {
+        if (b.zh != OOB) b.zh = zf_boundary<R, RZ>(L, b.bid, false, lx, ly);
+        if (b.zd) b.zh = zf_boundary<R, RZ>(L, b.bid, true, lx, ly);
+    } else if (b.zd) {
         const int zn = RZ ? zb * 8 - 1 : zb * 8 + 8;          // z-downwind node of the brick's last slot
         b.zh = ci.x + zoff_bytes<R>(zn >> 3) + (uint32_t)(zn & 7) * (uint32_t)sizeof(R);
     }
@@ -661,16 +671,17 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
 // (the ring then has nr = 2 + 16 / KB slots); 0: runtime L.kb / L.nr.
 // nchg: per-lane count of changed column segments (visit statistics).
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB, bool CMP>
-__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
+__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, Rsrc zfr, const BcBoxes &bc,
                                      const Smem<R, CMP> &S, int rx, int ry, int clock_it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
+    const Rsrc zr_ = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? zfr : ur;   // where the z-boundary nodes are read
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
     const R hr = (R)L.h;
     const int kb = KB > 0 ? KB : L.kb;
-    const int nr = KB > 0 ? 2 + (16 + KB - 1) / KB : L.nr;
+    const int nr = KB > 0 ? 2 + (16 + KB - 1) / (KB > 0 ? KB : 1) : L.nr;
 
     // halo loader role of this lane (halo_edge_lane)
     const int hj = lane >> 1, hh = lane & 1, he = halo_edge_lane(hj), hd = (he & 7) + (he >> 3);
@@ -763,7 +774,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         bload4(ur, ho, hq);
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
-    zc = bload1(ur, b0.zh, R());
+    zc = bload1(zr_, b0.zh, R());
     TRAF(S, 0, b0.seg != OOB, 8 * sizeof(R));
     TRAF(S, 2, b0.zh != OOB, sizeof(R));
     pos_adv(p3, kb, nr);
@@ -775,7 +786,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         bload4(ur, ho, hn);   // halos of vb+1
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
-    zn = bload1(ur, b1.zh, R());
+    zn = bload1(zr_, b1.zh, R());
     TRAF(S, 0, b1.seg != OOB, 8 * sizeof(R));
     TRAF(S, 2, b1.zh != OOB, sizeof(R));
     BInfo b2;
@@ -783,7 +794,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         pos_adv(p3, kb, nr);
         b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, cinfo_at(L, S, p3.ri, lane, lanecol));
         bload8(ur, b2.seg, q);
-        zq = bload1(ur, b2.zh, R());
+        zq = bload1(zr_, b2.zh, R());
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -895,7 +906,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, ci3);
         if (AH == 3) {
             bload8(ur, b3.seg, p);
-            zp = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
+            zp = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(zr_, b3.zh, R()) : R(0);
         } else {
             if (PAIR)
                 pair_issue(ur, b3.seg, qa, qb);
@@ -903,7 +914,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
                 line_issue64(ur, b3.lseg, p3.vb >= 0 && (p3.zbs & 1) == 0, la, lh, rowl, rowo);
             else
                 bload8(ur, b3.seg, q);
-            zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(ur, b3.zh, R()) : R(0);
+            zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(zr_, b3.zh, R()) : R(0);
         }
         {
             const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, cie, hbit, hdelta);
@@ -1015,10 +1026,13 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if constexpr (HOLD) {
             // what this lane changed: the block, its x / y faces (edge columns), its z faces (the
             // block's lowest / highest node of the column)
-            if (changed) {
-                const int zr = (b0.zb8 >> 3) % kb;                 // brick index in the block
-                const unsigned m = xyface | ((zr == 0 && c0) ? HOLD_ZLO : 0u) | ((zr == kb - 1 && c7) ? HOLD_ZHI : 0u);
-                atomicOr(&S.fmask[b0.ri], m);
+            const int zr = (b0.zb8 >> 3) % kb;                     // brick index in the block
+            const bool zlo = changed && zr == 0 && c0, zhi = changed && zr == kb - 1 && c7;
+            if (changed) atomicOr(&S.fmask[b0.ri], xyface | (zlo ? HOLD_ZLO : 0u) | (zhi ? HOLD_ZHI : 0u));
+            // the block's lowest / highest node of this column changed: its z-face copy too
+            if (MCEIK8_ZF && __any(zlo || zhi)) {
+                bstore1(zfr, zlo ? zf_off<R>(b0.bid, 0, lx, ly) : OOB, r[0]);
+                bstore1(zfr, zhi ? zf_off<R>(b0.bid, 1, lx, ly) : OOB, r[7]);
             }
         } else if (changed) {
             S.lastchg[b0.bid] = (typename Smem<R, CMP>::clk_t)(clock0 + b0.clk);   // lanes of one block write the same value
@@ -1201,6 +1215,8 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             slow_bytes = (uint32_t)(ncell * 4);
         }
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
+        const size_t zfb = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? zf_bytes(L, sizeof(R)) : 0;
+        const Rsrc zfr = make_rsrc(reinterpret_cast<char *>(L.zf) + (size_t)blockIdx.x * zfb, (uint32_t)zfb);
         // Clocks before the first sweep: every block "visited" at -2 and
         // unchanged since (-3), except the blocks holding boundary-condition
         // nodes (changed at -1).  Exact: a block whose nodes and neighbours
@@ -1227,6 +1243,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
         if constexpr (HOLD) {
             hold_solve_start(L, hold_lds(S), bc, L.nr);
+            if (MCEIK8_ZF) zf_init<R>(L, zfr, u, bc);
         } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
@@ -1259,10 +1276,12 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
                         clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg, nsteps);
+                                              L, ur, u0r, sr, zfr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
+                                              nsteps);
                     else
                         clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg, nsteps);
+                                              L, ur, u0r, sr, zfr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
+                                              nsteps);
 #ifdef MCEIK_STEPSTATS
                     {   // experiment: visited blocks of this sweep that did not change
                         const int c1 = clock - L.infl;
