@@ -229,7 +229,9 @@ def test_c5_fields_within_fp32_tolerance_of_reference():
     assert not fails, fails
 
 
-ACCEPT_FLOOR = 0.99          # identical accept decisions, fp32 vs fp64 sampler
+# identical accept decisions, fp32 vs fp64 sampler: observed 0.99023 (50 of 5120 differ,
+# profiles/r05_a/gpu_tests_tolerance_phases_multistep.log); the floor leaves 2x that fraction of headroom
+ACCEPT_FLOOR = 0.98
 
 
 @pytest.mark.timeout(900)
