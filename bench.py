@@ -35,7 +35,7 @@ METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI3
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 # sweep-kernel revision per precision (bump when that kernel changes; the
 # profiles/traffic.json record of that precision must match)
-KERNEL_REVS = {32: "fsm-v35", 64: "fsm-v34"}
+KERNEL_REVS = {32: "fsm-v36", 64: "fsm-v35"}
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -130,20 +130,38 @@ def cpu_baseline(p, v0, cores, rounds=CPU_ROUNDS):
 
 
 def node_gpus():
-    """GPU agents of this host from the KFD topology (every GPU of the node,
-    whether or not this process may use it; sysfs only, no GPU call), or None."""
+    """(GPUs of this host, source) from sysfs only (no GPU call): the KFD
+    topology's GPU agents, else the PCI functions of AMD (0x1002) processing
+    accelerators / display controllers (every GPU of the node, whether or not
+    this process may use it); (None, None) when neither is readable."""
     base = "/sys/class/kfd/kfd/topology/nodes"
-    n = 0
     try:
+        n = 0
         for d in os.listdir(base):
             with open(os.path.join(base, d, "properties")) as f:
                 for line in f:
                     k, _, v = line.partition(" ")
                     if k == "simd_count" and int(v) > 0:
                         n += 1
+        if n:
+            return n, "kfd topology"
     except (OSError, ValueError):
-        return None
-    return n or None
+        pass
+    try:
+        n = 0
+        pci = "/sys/bus/pci/devices"
+        for d in os.listdir(pci):
+            with open(os.path.join(pci, d, "vendor")) as f:
+                vendor = f.read().strip()
+            with open(os.path.join(pci, d, "class")) as f:
+                cls = int(f.read().strip(), 16) >> 16
+            if vendor == "0x1002" and cls in (0x12, 0x03):     # processing accelerator / display controller
+                n += 1
+        if n:
+            return n, "pci (vendor 0x1002, class 0x12/0x03)"
+    except (OSError, ValueError):
+        pass
+    return None, None
 
 
 def core_share(cpu):
@@ -151,9 +169,10 @@ def core_share(cpu):
     GPUs on the node), next to the allotted `cores` the leg actually used;
     the share's rate assumes the reference's table-parallel solves scale
     linearly with cores (they are independent single-threaded solves)."""
-    host, ngpu = os.cpu_count() or 1, node_gpus()
+    host, (ngpu, src) = os.cpu_count() or 1, node_gpus()
     cpu["host_cpus"] = host
     cpu["gpus_on_node"] = ngpu
+    cpu["gpus_on_node_source"] = src
     if ngpu:
         share = host // ngpu
         cpu["per_gpu_share_cores"] = share

@@ -906,26 +906,26 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     constexpr bool HOLD = MCEIK16_HOLD;
-    HoldStream hs_;
-    hs_.done = 0; hs_.last = -1;
     const HoldLds<unsigned short> H = hold_lds16(S);
-    int nset = 0;                                    // held stream: positions settled so far
+    // (the held stream's scan state -- first incomplete tile, previous position's tile -- lives in LDS
+    // scratch [4], [5]: fewer scalar registers live across the step loop)
     // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
     // lane's column is a tile edge (absolute orientation)
     const unsigned xyface = HOLD_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
                             (ly == 7 ? 16u : 0u);
     if (HOLD) {
         hold_norm(L, H);
+        if (lane == 0) { S.scratch[4] = 0; S.scratch[5] = -1; }
         clock0 = 64;
     }
     // the next position's block (held stream: after settling the visit infl positions back)
     auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
         if (!HOLD) return decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
-        while (nset <= pos - g.infl) {
-            hold_settle(L, H, nset % nr, clock0 + nset);
-            nset++;
-        }
-        return hold_decide<RZ>(L, H, hs_, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, g.infl, g.vis, zh);
+        // positions are decided one after another: settle the one infl back
+        const int q = pos - g.infl;
+        if (q >= 0) hold_settle(L, H, q % nr, clock0 + q);
+        return hold_decide<RZ>(L, H, S.scratch + 4, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, g.infl, g.vis,
+                               zh);
     };
     constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
     constexpr bool LEAN = KB16 == 2 && MCEIK16_LEAN;     // lean position words (2-step positions)
@@ -1301,7 +1301,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     if (HOLD) {
         // the last visits' changes (every lane is past them)
-        for (; nset < nstream; nset++) hold_settle(L, H, nset % nr, clock0 + nset);
+        for (int q = max(0, nstream - g.infl + 1); q < nstream; q++) hold_settle(L, H, q % nr, clock0 + q);
     }
 #if defined(MCEIK_ADMIT_STATS) && !MCEIK16_HOLD
     admit_flush16(S, nr);

@@ -54,10 +54,8 @@ struct HoldLds {
     const int *ring_e;           // per ring slot: entry tx | ty << 12 | tz << 24, bubble -1
     unsigned *vbits, *cbits;     // blocks visited / changed in this iteration (bitmaps)
 };
-struct HoldStream {
-    int done;                    // tiles [0, done) of the diagonal order are complete
-    int last;                    // diagonal index of the previous position's tile, -1 none
-};
+// scan state (int [2] in LDS): [0] tiles [0, done) of the diagonal order are
+// complete, [1] diagonal index of the previous position's tile, -1 none
 enum { HOLD_DONE = 0, HOLD_BLOCKED, HOLD_HELD, HOLD_WAIT, HOLD_SKIP, HOLD_READY };
 
 template <typename OrderT>
@@ -116,12 +114,14 @@ __device__ __forceinline__ int hold_status(const FsmLaunch &L, const HoldLds<Ord
 // Progress: the first incomplete tile's upwind tiles are complete, so within
 // infl positions its next block is ready or skipped.
 template <bool RZ, typename OrderT>
-__device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<OrderT> &H, HoldStream &st, int C, int rx,
+__device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<OrderT> &H, int *sst, int C, int rx,
                                            int ry, int rprev, int infl, int vis, int &zh)
 {
     const int lane = threadIdx.x, nt = L.ntiles;
     zh = 0;
     int pick = -1, pid = 0, pk = 0, pro = 0;
+    asm volatile("" ::: "memory");
+    struct { int done, last; } st = {__builtin_amdgcn_readfirstlane(sst[0]), __builtin_amdgcn_readfirstlane(sst[1])};
     if (st.last >= 0) {
         int id, k, ro;
         const int s = hold_status<RZ>(L, H, st.last, C, rx, ry, infl, vis, id, k, ro);
@@ -142,7 +142,9 @@ __device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<Ord
             if (n < 64) break;
         }
         if (st.done >= nt) {
-            st.last = -1;
+            asm volatile("" ::: "memory");
+            if (lane == 0) { sst[0] = st.done; sst[1] = -1; }
+            asm volatile("" ::: "memory");
             return -2;
         }
         for (int base = st.done; base < nt && pick < 0; base += 64) {
@@ -166,17 +168,19 @@ __device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<Ord
             }
         }
     }
+    asm volatile("" ::: "memory");
     if (pick < 0) {
-        st.last = -1;
+        if (lane == 0) { sst[0] = st.done; sst[1] = -1; }
+        asm volatile("" ::: "memory");
         return -1;
     }
-    asm volatile("" ::: "memory");
     if (lane == 0) {
         H.fz[pid] = (unsigned char)(pk + 1);
         if (pro) atomicOr(&H.fmask[rprev], HOLD_CONT);   // the previous position's run continues here
+        sst[0] = st.done;
+        sst[1] = pick;
     }
     asm volatile("" ::: "memory");
-    st.last = pick;
     zh = pk > 0 && !pro;
     const int ty = pid / L.ntx, tx = pid - ty * L.ntx;
     return tx | (ty << 12) | ((RZ ? L.nzk - 1 - pk : pk) << 24);

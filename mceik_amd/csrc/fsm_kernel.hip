@@ -697,26 +697,26 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     // the held stream (compact layout; fsm_hold.h): clocks restart at 64 every sweep
     constexpr bool HOLD = CMP && MCEIK8_HOLD;
-    HoldStream hs_;
-    hs_.done = 0; hs_.last = -1;
-    int nset = 0;                                    // positions settled so far
+    // (its scan state -- first incomplete tile, previous position's tile -- lives in LDS scratch
+    // [4], [5]: fewer scalar registers live across the step loop)
     // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
     // lane's column is a tile edge (absolute orientation)
     const unsigned xyface = HOLD_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
                             (ly == 7 ? 16u : 0u);
     if constexpr (HOLD) {
         hold_norm(L, hold_lds(S));
+        if (lane == 0) { S.scratch[4] = 0; S.scratch[5] = -1; }
         clock0 = 64;
     }
     // the next position's block (held stream: after settling the visit infl positions back)
     auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
         if constexpr (HOLD) {
             const HoldLds<int> H = hold_lds(S);
-            while (nset <= pos - L.infl) {
-                hold_settle(L, H, nset % nr, clock0 + nset);
-                nset++;
-            }
-            return hold_decide<RZ>(L, H, hs_, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, L.infl, L.vis, zh);
+            // positions are decided one after another: settle the one infl back
+            const int q = pos - L.infl;
+            if (q >= 0) hold_settle(L, H, q % nr, clock0 + q);
+            return hold_decide<RZ>(L, H, S.scratch + 4, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, L.infl,
+                                   L.vis, zh);
         } else {
             return decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
         }
@@ -1089,7 +1089,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     if constexpr (HOLD) {
         // the last visits' changes (every lane is past them)
         const HoldLds<int> H = hold_lds(S);
-        for (; nset < nstream; nset++) hold_settle(L, H, nset % nr, clock0 + nset);
+        for (int q = max(0, nstream - L.infl + 1); q < nstream; q++) hold_settle(L, H, q % nr, clock0 + q);
     }
     return nstream;
 }
