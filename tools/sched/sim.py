@@ -99,6 +99,8 @@ class State:
 
 CONT = False
 PAR = False
+LEVEL = False
+FORCEK = None
 
 
 def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
@@ -218,9 +220,11 @@ def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
                     return "held", b, 0
                 return "skip", b, 0
 
+            nbub = 0
             while done < len(tiles):
                 S.settle(C)
                 chosen = None
+                heldc = None
                 if last_t is not None:
                     st_, b, r = status(last_t)
                     tot["checks"] += 1
@@ -236,7 +240,16 @@ def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
                         while True:
                             tot["rounds"] += 1
                             sts = [status(t) for t in win]
+                            if heldc is None:
+                                for i, x in enumerate(sts):
+                                    if x[0] == "held":
+                                        heldc = (win[i], x[1])
+                                        break
                             rdy = [i for i, x in enumerate(sts) if x[0] == "ready"]
+                            if LEVEL and rdy:
+                                # the ready block on the lowest hyperplane diag + k first
+                                rdy.sort(key=lambda i: (tindex[win[i]] and (win[i][0] if not rx else g.ntx - 1 - win[i][0])
+                                                        + (win[i][1] if not ry else g.nty - 1 - win[i][1])) + fz[win[i]])
                             skips = [i for i, x in enumerate(sts) if x[0] == "skip"]
                             for i in skips:
                                 fz[win[i]] += 1
@@ -249,12 +262,31 @@ def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
                         base += 64
                 while done < len(tiles) and fz[tiles[done]] == g.nzk:
                     done += 1
+                if chosen is None and FORCEK is not None and heldc is not None and nbub >= FORCEK:
+                    t, b = heldc
+                    # forced: visible only if its upwind visits are >= vis back
+                    tz = b // g.nt
+                    ok = True
+                    for dx, dy in ((1, 0), (0, 1)):
+                        u = up(t, dx, dy)
+                        if u is not None and S.lp[g.bid(u[0], u[1], tz)] + vis > C:
+                            ok = False
+                    k_ = zorder.index(tz)
+                    if k_ > 0:
+                        zb_ = g.bid(t[0], t[1], zorder[k_ - 1])
+                        if S.lp[zb_] != C - 1 and S.lp[zb_] + vis > C:
+                            ok = False
+                    if ok:
+                        chosen = (t, b, 4)
+                        tot["forced"] += 1
                 if chosen is None:
                     if done >= len(tiles):
                         break
                     tot["bubbles"] += 1
+                    nbub += 1
                     C += 1
                     continue
+                nbub = 0
                 t, b, r = chosen
                 admit(b, C, r)
                 last_t = t
@@ -339,10 +371,14 @@ def main():
     ap.add_argument("--cont", action="store_true", help="hold policies: the current run's next block first")
     ap.add_argument("--par", action="store_true", help="hold policies: the kernel's parallel scan (holdb only)")
     ap.add_argument("--kb", type=int, default=2, help="steps per position (fsm16: 2; the 8-z kernel: 4)")
+    ap.add_argument("--level", action="store_true", help="--par: the ready block of the lowest diag + k first")
+    ap.add_argument("--forcek", type=int, default=None, help="--par: after k bubbles in a row visit a held block")
     a = ap.parse_args()
-    global CONT, PAR
+    global CONT, PAR, LEVEL, FORCEK
     CONT = a.cont
     PAR = a.par
+    LEVEL = a.level
+    FORCEK = a.forcek
     R = np.load(a.rec)
     g = Geo(int(R["nx"]), int(R["ny"]), int(R["nz"]))
     nst = len(R["stations"])
