@@ -201,7 +201,7 @@ static int fsm_batch_waves_uncapped(const mceik_fsm_batch *b)
 
 // Workspace: [8 queue heads, 1 KiB][slow brick copy (mode 0)][u scratch][u0 scratch]
 struct WsLayout {
-    size_t counter, slow, u, u0, total;
+    size_t counter, slow, u, u0, zf, total;
     int nwaves;
 };
 
@@ -218,7 +218,7 @@ static WsLayout ws_layout(const mceik_fsm_batch *b)
     // fp32 fields are 67 MB, 2048 waves would need 275 GB).  Waves then take
     // several solves each from the queue.
     {
-        const size_t per_wave = L.field_elems * es + u0_slot_bytes(L, es);
+        const size_t per_wave = 2 * L.field_elems * es + zf_bytes(L, es);
         const long cap = (long)(ws_budget_bytes() / (per_wave ? per_wave : 1));
         if (cap >= 1 && w.nwaves > cap) w.nwaves = (int)cap;
     }
@@ -228,8 +228,8 @@ static WsLayout ws_layout(const mceik_fsm_batch *b)
     w.u = w.slow + ((slow_bytes + 255) & ~(size_t)255);
     size_t nu = b->u_out ? (size_t)L.nsolve : (size_t)w.nwaves;
     w.u0 = w.u + nu * L.field_elems * es;
-    w.u0 = (w.u0 + 255) & ~(size_t)255;
-    w.total = w.u0 + (size_t)w.nwaves * u0_slot_bytes(L, es);      // u0 + the held stream's z-face copies
+    w.zf = w.u0 + (size_t)w.nwaves * L.field_elems * es;          // the held stream's z-face copies
+    w.total = w.zf + (size_t)w.nwaves * zf_bytes(L, es);
     return w;
 }
 
@@ -303,8 +303,8 @@ static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_
     {
         FsmLaunch G;
         fill_launch(G, b);
-        if (u0_slot_bytes(G, b->precision == 64 ? 8 : 4) >= (size_t)1 << 31) {
-            fprintf(stderr, "mceik_fsm_batch_solve: one travel-time field (+ its z-face copies) must stay below 2 GiB\n");
+        if (G.field_elems * (b->precision == 64 ? 8 : 4) >= (size_t)1 << 31) {
+            fprintf(stderr, "mceik_fsm_batch_solve: one travel-time field must stay below 2 GiB\n");
             return 1;
         }
         if (fsm_launch_lds_bytes(G, b->precision == 64) > MCEIK_MAX_LDS) {
@@ -341,7 +341,7 @@ static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_
     }
     L.u = ws + w.u;
     L.u0 = ws + w.u0;
-    L.u0_stride = u0_slot_bytes(L, is_double ? 8 : 4);
+    L.zf = ws + w.zf;
     L.slot_per_solve = b->u_out ? 1 : 0;
     if (ext) {
         if (is_double || fsm_launch_kind(L, 0) != 16 || b->solve_order || b->u_out) return 1;

@@ -884,13 +884,11 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
 // 16-z bricks and the brick values updated in place: a lane's next brick
 // lives in its XN row and is read back into v at the end of the step.
 template <bool RZ, int KB16, int CCR>
-__device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr,
+__device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rsrc ur, Rsrc u0r, Rsrc sr, Rsrc zfr,
                                        const BcBoxes &bc, const Smem16 &S, int rx, int ry, int clock0, bool &notconv,
                                        int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
-    // where the z-boundary nodes are read: the z-face copies in the wave's u0 slot (held stream)
-    const Rsrc zr_ = MCEIK16_HOLD ? u0r : ur;
-    const uint32_t zfb0 = (uint32_t)u0_field_bytes(L, 4);
+    const Rsrc zr_ = MCEIK16_HOLD ? zfr : ur;        // where the z-boundary nodes are read
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const float UN = FLT_MAX;
@@ -1179,10 +1177,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         }
         const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
         bool changed = false, nc = false, c0 = false, c15 = false;
-        // (no lane on a z-block -- every position in the lanes' window a bubble or past the stream's
-        // end: the update's results would be discarded, so it is not computed)
-        if (MCEIK_IDLE_SKIP && !__any(b0.fl() & F_VALID)) {
-        } else if (__any(b0.fl() & F_SLOW))
+        if (__any(b0.fl() & F_SLOW))
             brick16<RZ, true, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
         else
             brick16<RZ, false, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
@@ -1270,8 +1265,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             if (changed) atomicOr(&S.fmask[b0.ri()], xyface | (zlo ? HOLD_ZLO : 0u) | (zhi ? HOLD_ZHI : 0u));
             // the block's lowest / highest node of this column changed: its z-face copy too
             if (__any(zlo || zhi)) {
-                bstore1(u0r, zlo ? zfb0 + zf_off<float>(b0.bid(), 0, lx, ly) : OOB, v[0]);
-                bstore1(u0r, zhi ? zfb0 + zf_off<float>(b0.bid(), 1, lx, ly) : OOB, v[15]);
+                bstore1(zfr, zlo ? zf_off<float>(b0.bid(), 0, lx, ly) : OOB, v[0]);
+                bstore1(zfr, zhi ? zf_off<float>(b0.bid(), 1, lx, ly) : OOB, v[15]);
             }
         } else if (changed) {
             S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
@@ -1540,7 +1535,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         const int model = (int)solve / L.nstat, station = (int)solve - model * L.nstat;
         const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
         float *u = reinterpret_cast<float *>(L.u) + slot * L.field_elems;
-        float *u0 = reinterpret_cast<float *>(reinterpret_cast<char *>(L.u0) + (size_t)blockIdx.x * L.u0_stride);
+        float *u0 = reinterpret_cast<float *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
         const size_t ncell = (size_t)L.ncx * L.ncy * L.ncz;
         // (a multi-step launch's model phase changes between steps: vector load)
         const int phase = L.model_phase ? (MC ? mcmcd::ldv(L.model_phase + model) : L.model_phase[model])
@@ -1554,9 +1549,10 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         }
         const size_t sentry = !L.model_phase ? (size_t)model : (size_t)model * L.nphase + phase;
         const void *slow_model = reinterpret_cast<const float *>(L.slow) + sentry * ncell;
-        // (the u0 slot: the side field, then the held stream's z-face copies)
-        const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, (uint32_t)L.u0_stride),
+        const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
                    sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
+        const size_t zfb = MCEIK16_HOLD ? zf_bytes(L, 4) : 0;
+        const Rsrc zfr = make_rsrc(reinterpret_cast<char *>(L.zf) + (size_t)blockIdx.x * zfb, (uint32_t)zfb);
         // Before the first sweep every block counts as visited and unchanged
         // (lastproc 2 > lastchg 1) except the blocks holding boundary-condition
         // nodes (lastchg 3): a block whose nodes and neighbours are all u_nan
@@ -1580,7 +1576,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         const bool ok = init_field<float, 1>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
         if (MCEIK16_HOLD) {
             hold_solve_start(L, hold_lds16(S), bc, g.nr);
-            zf_init<float>(L, u0r, u, bc);
+            zf_init<float>(L, zfr, u, bc);
         } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
@@ -1607,10 +1603,10 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
                     // positions used + a gap of infl: the previous sweep's visits are
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
-                        clock += g.infl + sweep16<true, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                        clock += g.infl + sweep16<true, KB16, CCR>(L, g, ur, u0r, sr, zfr, bc, S, rx, ry, clock, notconv,
                                                               ierr_last, nchg, nsteps);
                     else
-                        clock += g.infl + sweep16<false, KB16, CCR>(L, g, ur, u0r, sr, bc, S, rx, ry, clock, notconv,
+                        clock += g.infl + sweep16<false, KB16, CCR>(L, g, ur, u0r, sr, zfr, bc, S, rx, ry, clock, notconv,
                                                                ierr_last, nchg, nsteps);
                     __builtin_amdgcn_s_waitcnt(0);      // stores of this sweep land before the next sweep's loads
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

@@ -37,11 +37,10 @@ struct FsmLaunch {
     int nzq;                     // 128-B line groups per column: ceil(nzb / (16 / es))
     size_t field_elems;          // ntiles * nzq * 64 * (128 / es)
     void *u;                     // travel-time fields (brick layout, R)
-    size_t u0_stride;            // bytes of one wave's u0 slot (u0_slot_bytes)
-    void *u0;                    // per-wave slots of u0_slot_bytes: the convergence side field (same layout
-                                 // as u), then (held stream) the z-face copies: every z-block's lowest and
-                                 // highest node per column, [nblocks][2][64 columns lx + 8 ly] R, the values a
-                                 // run start / end reads across a z-block boundary
+    void *u0;                    // convergence side field (same layout)
+    void *zf;                    // held stream: per-wave copies of every z-block's lowest and highest node per
+                                 // column, [nblocks][2][64 columns lx + 8 ly] R (zf_bytes), the values a run
+                                 // start / end reads across a z-block boundary
     int slot_per_solve;          // 1: field slot = solve id; 0: slot = blockIdx.x (scratch)
     const int *ev_node;          // event nodes (x-fastest linear index), may be null
     int nev;
@@ -92,21 +91,8 @@ static inline __host__ __device__ size_t fsm_slow_entry(const FsmLaunch &L, int 
 }
 
 static inline __host__ __device__ int mceik_div_up(int a, int b) { return (a + b - 1) / b; }
-// skip a step's brick update when no lane holds a z-block (the sweep kernels): off, measured 0.8% slower
-// in fp32 (profiles/r05_ab2: such steps are rare, the branch costs registers)
-#ifndef MCEIK_IDLE_SKIP
-#define MCEIK_IDLE_SKIP 0
-#endif
-// one wave's u0 slot: the side field, then the z-face copies (FsmLaunch.u0)
+// bytes of one wave's z-face copies (FsmLaunch.zf)
 static inline __host__ __device__ size_t zf_bytes(const FsmLaunch &L, size_t es) { return (size_t)L.nblocks * 128 * es; }
-static inline __host__ __device__ size_t u0_field_bytes(const FsmLaunch &L, size_t es)
-{
-    return (L.field_elems * es + 255) & ~(size_t)255;    // = the z-face copies' offset in the slot
-}
-static inline __host__ __device__ size_t u0_slot_bytes(const FsmLaunch &L, size_t es)
-{
-    return u0_field_bytes(L, es) + zf_bytes(L, es);
-}
 
 // Debug / accounting counters in LDS: [0..3] visit statistics; MCEIK_TRAFFIC
 // builds add [8..15], the requested global-memory bytes of the wave's current

@@ -294,24 +294,22 @@ __device__ __forceinline__ uint32_t zf_boundary(const FsmLaunch &L, int b, bool 
 {
     // sweep z ascending: below = tz - 1 (its highest node), above = tz + 1 (its lowest)
     const bool up = zd != RZ;                               // the neighbour is at tz + 1
-    return (uint32_t)u0_field_bytes(L, sizeof(R)) + zf_off<R>(b + (up ? L.ntiles : -L.ntiles), up ? 0 : 1, lx, ly);
+    return zf_off<R>(b + (up ? L.ntiles : -L.ntiles), up ? 0 : 1, lx, ly);
 }
 // Start of a solve (after init_field, whose stores have completed): every
 // copy is u_nan except the boundary-condition nodes on a block's lowest or
 // highest layer, copied from the field (lanes 0-26: the 3 x 3 x 3 candidate
-// nodes of each source box).  u0r: the wave's u0 slot, whose copies start at
-// u0_field_bytes.
+// nodes of each source box).
 template <typename R>
-__device__ __forceinline__ void zf_init(const FsmLaunch &L, Rsrc u0r, const R *u, const BcBoxes &bc)
+__device__ __forceinline__ void zf_init(const FsmLaunch &L, Rsrc zfr, const R *u, const BcBoxes &bc)
 {
     const int lane = threadIdx.x;
     const R UN = Num<R>::unan();
     R fill[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) fill[i] = UN;
-    const uint32_t zb0 = (uint32_t)u0_field_bytes(L, sizeof(R));
     const uint32_t nvec = (uint32_t)(zf_bytes(L, sizeof(R)) / (8 * sizeof(R)));
-    for (uint32_t i = lane; i < nvec; i += 64) bstore8(u0r, zb0 + i * 8u * (uint32_t)sizeof(R), fill);
+    for (uint32_t i = lane; i < nvec; i += 64) bstore8(zfr, i * 8u * (uint32_t)sizeof(R), fill);
     __builtin_amdgcn_s_waitcnt(0);
     const int zbk = 8 * L.kb;                                  // z per block
     for (int s = 0; s < bc.n; s++) {
@@ -321,7 +319,7 @@ __device__ __forceinline__ void zf_init(const FsmLaunch &L, Rsrc u0r, const R *u
             const int zr = z % zbk;
             if (zr == 0 || zr == zbk - 1) {
                 const int b = ((z / zbk) * L.nty + (y >> 3)) * L.ntx + (x >> 3);
-                bstore1(u0r, zb0 + zf_off<R>(b, zr == 0 ? 0 : 1, x & 7, y & 7), u[brick_index<R>(L, x, y, z)]);
+                bstore1(zfr, zf_off<R>(b, zr == 0 ? 0 : 1, x & 7, y & 7), u[brick_index<R>(L, x, y, z)]);
             }
         }
     }

@@ -671,13 +671,11 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
 // (the ring then has nr = 2 + 16 / KB slots); 0: runtime L.kb / L.nr.
 // nchg: per-lane count of changed column segments (visit statistics).
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB, bool CMP>
-__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
+__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, Rsrc zfr, const BcBoxes &bc,
                                      const Smem<R, CMP> &S, int rx, int ry, int clock_it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
-    // where the z-boundary nodes are read: the z-face copies in the wave's u0 slot, or the field
-    const Rsrc zr_ = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? u0r : ur;
-    const uint32_t zfb0 = (uint32_t)u0_field_bytes(L, sizeof(R));
+    const Rsrc zr_ = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? zfr : ur;   // where the z-boundary nodes are read
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
@@ -931,10 +929,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         // one loaded from HBM)
         bool changed = false, nc = false, c0 = false, c7 = false;
         const bool zdsel = HOLD && b0.zd && !(S.fmask[b0.ri] & HOLD_CONT);
-        // (no lane on a z-block -- every position in the lanes' window a bubble or past the stream's
-        // end: the update's results would be discarded, so it is not computed)
-        if (MCEIK_IDLE_SKIP && !__any(b0.fl & F_VALID)) {
-        } else if (__any(b0.fl & F_SLOW))
+        if (__any(b0.fl & F_SLOW))
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                            ierr_last, zdsel, c0, c7);
         else
@@ -1036,8 +1031,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             if (changed) atomicOr(&S.fmask[b0.ri], xyface | (zlo ? HOLD_ZLO : 0u) | (zhi ? HOLD_ZHI : 0u));
             // the block's lowest / highest node of this column changed: its z-face copy too
             if (MCEIK8_ZF && __any(zlo || zhi)) {
-                bstore1(u0r, zlo ? zfb0 + zf_off<R>(b0.bid, 0, lx, ly) : OOB, r[0]);
-                bstore1(u0r, zhi ? zfb0 + zf_off<R>(b0.bid, 1, lx, ly) : OOB, r[7]);
+                bstore1(zfr, zlo ? zf_off<R>(b0.bid, 0, lx, ly) : OOB, r[0]);
+                bstore1(zfr, zhi ? zf_off<R>(b0.bid, 1, lx, ly) : OOB, r[7]);
             }
         } else if (changed) {
             S.lastchg[b0.bid] = (typename Smem<R, CMP>::clk_t)(clock0 + b0.clk);   // lanes of one block write the same value
@@ -1208,7 +1203,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         }
         const size_t slot = L.slot_per_solve ? solve : blockIdx.x;
         R *u = reinterpret_cast<R *>(L.u) + slot * L.field_elems;
-        R *u0 = reinterpret_cast<R *>(reinterpret_cast<char *>(L.u0) + (size_t)blockIdx.x * L.u0_stride);
+        R *u0 = reinterpret_cast<R *>(L.u0) + (size_t)blockIdx.x * L.field_elems;   // per-wave scratch
         const void *slow_model;
         uint32_t slow_bytes;
         if (SLOWMODE == 0) {
@@ -1219,9 +1214,9 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             slow_model = reinterpret_cast<const float *>(L.slow) + fsm_slow_entry(L, model) * ncell;
             slow_bytes = (uint32_t)(ncell * 4);
         }
-        // (the u0 slot: the side field, then the held stream's z-face copies)
-        const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, (uint32_t)L.u0_stride),
-                   sr = make_rsrc(slow_model, slow_bytes);
+        const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
+        const size_t zfb = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? zf_bytes(L, sizeof(R)) : 0;
+        const Rsrc zfr = make_rsrc(reinterpret_cast<char *>(L.zf) + (size_t)blockIdx.x * zfb, (uint32_t)zfb);
         // Clocks before the first sweep: every block "visited" at -2 and
         // unchanged since (-3), except the blocks holding boundary-condition
         // nodes (changed at -1).  Exact: a block whose nodes and neighbours
@@ -1248,7 +1243,7 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
         if constexpr (HOLD) {
             hold_solve_start(L, hold_lds(S), bc, L.nr);
-            if (MCEIK8_ZF) zf_init<R>(L, u0r, u, bc);
+            if (MCEIK8_ZF) zf_init<R>(L, zfr, u, bc);
         } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
@@ -1281,11 +1276,11 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
                         clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
+                                              L, ur, u0r, sr, zfr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
                                               nsteps);
                     else
                         clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
+                                              L, ur, u0r, sr, zfr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
                                               nsteps);
 #ifdef MCEIK_STEPSTATS
                     {   // experiment: visited blocks of this sweep that did not change
