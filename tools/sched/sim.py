@@ -371,6 +371,7 @@ def main():
     ap.add_argument("--cont", action="store_true", help="hold policies: the current run's next block first")
     ap.add_argument("--par", action="store_true", help="hold policies: the kernel's parallel scan (holdb only)")
     ap.add_argument("--kb", type=int, default=2, help="steps per position (fsm16: 2; the 8-z kernel: 4)")
+    ap.add_argument("--infl", type=int, default=0, help="positions a visit stays in flight (0: the kernel's 1 + ceil(16 / kb))")
     ap.add_argument("--level", action="store_true", help="--par: the ready block of the lowest diag + k first")
     ap.add_argument("--forcek", type=int, default=None, help="--par: after k bubbles in a row visit a held block")
     a = ap.parse_args()
@@ -387,7 +388,8 @@ def main():
         acc = None
         for k in range(nst):
             ah = 2
-            t = run(R[f"chg{k}"], R[f"face{k}"], R[f"bc{k}"], g, pol, kb=a.kb, infl=1 + -(-(14 + ah) // a.kb),
+            t = run(R[f"chg{k}"], R[f"face{k}"], R[f"bc{k}"], g, pol, kb=a.kb,
+                    infl=a.infl or 1 + -(-(14 + ah) // a.kb),
                     vis=-(-12 // a.kb))
             acc = t if acc is None else {key: (acc[key] + t[key] if not isinstance(t[key], list)
                                                else [x + y for x, y in zip(acc[key], t[key])]) for key in t}
