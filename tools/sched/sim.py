@@ -82,7 +82,7 @@ class State:
             _, b, c, f, clk = self.pending.popleft()
             if c:
                 self.chg[b] = clk
-                self.fchg[b, f] = clk
+            self.fchg[b, f] = clk             # (faces change only with the block)
 
     def reason(self, b):
         lp = self.lp[b]
@@ -103,7 +103,11 @@ LEVEL = False
 FORCEK = None
 
 
-def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
+def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6, rel=None):
+    """rel: (own_rel, face_rel) of record.py --rel: the marks a visit leaves
+    for later decisions (its own revisit, its face neighbours) follow the
+    relevance rule instead of every change; exactness is still asserted
+    against the actual changes."""
     face_rule = policy.endswith("+face") or policy == "face"
     base = "cur" if policy == "face" else policy.replace("+face", "")
     S = State(g, bc, face_rule)
@@ -115,6 +119,7 @@ def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
     for s in range(nsweep):
         rx, ry, rz = SWEEPS[s % 8]
         chg_s, face_s = rec_chg[s], rec_face[s]
+        mark_s, mface_s = (chg_s, face_s) if rel is None else (rel[0][s], rel[1][s])
         visited = np.zeros(g.nb, bool)
         last_admit = [None]
         zorder = list(range(g.nzk))[::-1] if rz else list(range(g.nzk))
@@ -145,7 +150,7 @@ def run(rec_chg, rec_face, bc, g, policy, kb=2, infl=9, vis=6):
             visited[b] = True
             S.lp[b] = C
             c = bool(chg_s[b])
-            S.pending.append((C + infl, b, c, face_s[b].copy(), C))
+            S.pending.append((C + infl, b, bool(mark_s[b]), mface_s[b].copy(), C))
             why[r] += 1
             why_chg[r] += c
             tot["visits"] += 1
@@ -371,6 +376,7 @@ def main():
     ap.add_argument("--cont", action="store_true", help="hold policies: the current run's next block first")
     ap.add_argument("--par", action="store_true", help="hold policies: the kernel's parallel scan (holdb only)")
     ap.add_argument("--kb", type=int, default=2, help="steps per position (fsm16: 2; the 8-z kernel: 4)")
+    ap.add_argument("--rel", action="store_true", help="marks by the relevance rule (record.py --rel)")
     ap.add_argument("--infl", type=int, default=0, help="positions a visit stays in flight (0: the kernel's 1 + ceil(16 / kb))")
     ap.add_argument("--level", action="store_true", help="--par: the ready block of the lowest diag + k first")
     ap.add_argument("--forcek", type=int, default=None, help="--par: after k bubbles in a row visit a held block")
@@ -390,7 +396,7 @@ def main():
             ah = 2
             t = run(R[f"chg{k}"], R[f"face{k}"], R[f"bc{k}"], g, pol, kb=a.kb,
                     infl=a.infl or 1 + -(-(14 + ah) // a.kb),
-                    vis=-(-12 // a.kb))
+                    vis=-(-12 // a.kb), rel=(R[f"own_rel{k}"], R[f"face_rel{k}"]) if a.rel else None)
             acc = t if acc is None else {key: (acc[key] + t[key] if not isinstance(t[key], list)
                                                else [x + y for x, y in zip(acc[key], t[key])]) for key in t}
         agg[pol] = acc
