@@ -139,6 +139,9 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 #ifndef MCEIK16_NPASS
 #define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
 #endif
+#ifndef MCEIK16_NC_SKIP
+#define MCEIK16_NC_SKIP 1        // no nc tests / u0 copies once the iteration is known unconverged (brick16)
+#endif
 #ifndef MCEIK16_HOLD
 #define MCEIK16_HOLD 1           // the held stream (fsm_hold.h): face-level change marks, blocks with an
                                  // in-flight dependency and no settled reason wait instead of being visited
@@ -783,7 +786,11 @@ __device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
 // fsm_kernel.hip brick_update (grid-edge columns of cut tiles, cut z-bricks,
 // BC nodes, node (0,0,0)); otherwise every lane's missing x/y neighbours are
 // already its own old values (the halo of a grid-edge lane is its column).
-template <bool RZ, bool GENERIC, bool LEAN>
+// NC: evaluate the "changed while >= T" test (nc).  Once a lane of the wave
+// has found the iteration unconverged, the test cannot change the outcome
+// (the iteration runs again, its verify and u0 copies are not used), so the
+// sweep drops it for the rest of the iteration (MCEIK16_NC_SKIP).
+template <bool RZ, bool GENERIC, bool LEAN, bool NC = true>
 __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, const BInfo16 &b0, float (&v)[16],
                                         float zprev0, float znext, int lx, int ly, int rx, int ry, bool &changed,
                                         bool &nc, int &ierr_last, bool &c0, bool &c15)
@@ -868,7 +875,7 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
                 nv = fmin_(self, godunov_v<true>(ux, uy, uz, fc, ffc, ff2c, ff3c));
             }
             const bool dec = nv < self;
-            nc |= dec && self >= T;
+            if (NC) nc |= dec && self >= T;
             changed |= dec;
             if (pj == 0) c0 = dec;                          // the brick's lowest / highest node changed
             if (pj == 15) c15 = dec;                        //   (z faces of its block, held stream)
@@ -1156,8 +1163,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             TRAF(S, 0, b3.seg != OOB, 64);
             TRAF(S, 2, b3.zh != OOB, 4);
         }
-        // ---- u0: old values of a block's first visit in the iteration (< T only)
-        if (__any(b0.fl() & C_U0)) {
+        // ---- u0: old values of a block's first visit in the iteration (< T only); none once the
+        // iteration is known unconverged (the verify that reads them does not run)
+        const bool wnc = !MCEIK16_NC_SKIP || !__any(notconv);
+        if (wnc && __any(b0.fl() & C_U0)) {
             unsigned m = __builtin_bit_cast(unsigned, v[0]);
 #pragma unroll
             for (int i = 1; i < 16; i++) m = min(m, __builtin_bit_cast(unsigned, v[i]));
@@ -1179,8 +1188,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         bool changed = false, nc = false, c0 = false, c15 = false;
         if (__any(b0.fl() & F_SLOW))
             brick16<RZ, true, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
-        else
+        else if (wnc)
             brick16<RZ, false, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
+        else
+            brick16<RZ, false, LEAN, false>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
 #ifdef MCEIK_EXP_VALU
         {   // sensitivity experiment: N extra dependent VALU per step (results unchanged)
             unsigned x = (unsigned)B;

@@ -32,6 +32,10 @@
 #endif
 // ... with its z-boundary nodes from the z-face copies (FsmLaunch.zf) instead of the field: off, measured
 // 2.4% slower in fp64 (the copies' stores and their buffer descriptor spill registers; profiles/r05_zf)
+// the step's unconverged test only until the iteration is known unconverged (brick_update NC)
+#ifndef MCEIK8_NC_SKIP
+#define MCEIK8_NC_SKIP 1
+#endif
 #ifndef MCEIK8_ZF
 #define MCEIK8_ZF 0
 #endif
@@ -560,7 +564,10 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R, CMP>
 // ierr); otherwise the brick is interior to the grid in x, y and z up to the
 // sweep-order first/last brick, no lane holds a BC node, and every lane's
 // missing x/y neighbours are already its own old values (column_info).
-template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC, bool CMP>
+// NC: evaluate the unconverged test (nc); the sweep drops it once a lane of
+// the wave has found the iteration unconverged (MCEIK8_NC_SKIP: the outcome
+// cannot change, as for the u0 copies under MCEIK_BIGSTEP)
+template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC, bool CMP, bool NC = true>
 __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, CMP> &S, const BInfo &b0, R (&c)[8],
                                              R (&n)[8], R (&r)[8], R zc, int lx, int ly, int rx, int ry,
                                              bool &changed, bool &nc, int &ierr_last, bool zdsel, bool &c0,
@@ -656,7 +663,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
             nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv, ffv, CELLF ? ff2c : ffv + ffv, CELLF ? ff3c : (R)3 * ffv));
         }
         const bool dec = nv < self;
-        nc |= dec && (self >= T || (MCEIK_BIGSTEP && sizeof(R) == 8 && self - nv >= TB));
+        if (NC) nc |= dec && (self >= T || (MCEIK_BIGSTEP && sizeof(R) == 8 && self - nv >= TB));
         changed |= dec;
         if (pj == 0) c0 = dec;               // the brick's lowest / highest node changed (z faces of
         if (pj == 7) c7 = dec;               //   its block, held stream)
@@ -932,9 +939,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (__any(b0.fl & F_SLOW))
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                            ierr_last, zdsel, c0, c7);
-        else
+        else if (!MCEIK8_NC_SKIP || !__any(notconv))
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, false>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                             ierr_last, zdsel, c0, c7);
+        else
+            brick_update<R, SLOWMODE, FAST, RZ, ZSH, false, CMP, false>(L, S, b0, c, n, r, zc, lx, ly, rx, ry,
+                                                                        changed, nc, ierr_last, zdsel, c0, c7);
         const bool val = (b0.fl & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
