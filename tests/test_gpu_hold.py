@@ -120,3 +120,29 @@ def test_held_stream_maxit_cut(precision, maxit):
     assert out["step_z"] == (16 if precision == 32 else 8)
     _check(out, scell, src, nx, ny, nz, precision, maxit)
     assert int(out["niter"].max()) == maxit
+
+
+def test_held_stream_runtime_kb_budgets():
+    """The runtime-kb instance of the 16-z kernel (C5's: 136 x 136 x 128 has
+    more z-blocks of 32 z than the LDS block tables hold, so the stream runs
+    64-z blocks): partial fields after a spread of sweep budgets, bitwise =
+    the full-sweep twin."""
+    dev = _dev()
+    nx = ny = 136
+    nz = 128
+    scell, src = _problem(nx, ny, nz, 2, 59)
+    scell, src = scell[1:], src[:1]                    # the fast-channel model, one station
+    bs = _batch(nx, ny, nz, 32, 50)
+    sl = torch.tensor(scell.reshape(1, -1), device=dev)
+    full = bs.solve(torch.tensor(src), sl, want_fields=True)
+    assert full["step_z"] == 16
+    import ctypes as C
+    from mceik_amd import _lib
+    kname = _lib.lib().mceik_fsm_kernel_name(C.byref(bs.describe(1, 1, 1, 1))).decode()
+    assert kname.startswith("fsm16_solve_kernel<0"), kname       # runtime kb
+    _check(full, scell, src, nx, ny, nz, 32, 50)
+    nsw = 8 * int(full["niter"].max())
+    for ms in sorted({1, 2, 3, 5, 8, 9, 13, 16, 21, nsw // 2, nsw - 1}):
+        if ms < nsw:
+            out = bs.solve(torch.tensor(src), sl, want_fields=True, max_sweeps=ms)
+            _check(out, scell, src, nx, ny, nz, 32, 50, max_sweeps=ms)
