@@ -146,3 +146,32 @@ def test_held_stream_runtime_kb_budgets():
         if ms < nsw:
             out = bs.solve(torch.tensor(src), sl, want_fields=True, max_sweeps=ms)
             _check(out, scell, src, nx, ny, nz, 32, 50, max_sweeps=ms)
+
+
+@pytest.mark.parametrize("precision", [32, 64], ids=["fp32_fsm16", "fp64_compact"])
+@pytest.mark.parametrize("tol", [1e-3, 1e-12], ids=["tol1e-3", "tol1e-12"])
+def test_convergence_paths_tol(precision, tol):
+    """The convergence test's two paths under the held stream: with tol 1e-3
+    no update is big enough to prove an iteration unconverged on its own
+    (fp32: T = tol 2^24 s exceeds every travel time), so every iteration
+    ends in the verify against the u0 copies; with tol 1e-12 nearly every
+    change proves it, and once a wave knows, the rest of the iteration runs
+    without the test or the u0 copies (MCEIK16_NC_SKIP / MCEIK8_NC_SKIP).
+    Fields, iterations and ierr bitwise = the twin either way."""
+    dev = _dev()
+    nx, ny, nz = 30, 26, 67
+    scell, src = _problem(nx, ny, nz, 2, 71)
+    from mceik_amd.eikonal import BatchSolver
+    bs = BatchSolver(nx, ny, nz, H, 0.0, 0.0, 0.0, 50, tol, precision, nref=NREF, fast_sqrt=True)
+    out = bs.solve(torch.tensor(src), torch.tensor(scell.reshape(2, -1), device=dev), want_fields=True,
+                   max_waves=1)
+    ut = np.uint32 if precision == 32 else np.uint64
+    dt = np.float32 if precision == 32 else np.float64
+    u = out["u"].cpu().numpy().reshape(4, -1)
+    for m in range(2):
+        sfield = _expand(scell[m], nx, ny, nz).astype(dt)
+        for s in range(2):
+            t, ierr, it = O.eikonal_solve(nx, ny, nz, sfield, H, src[s], maxit=50, tol=tol, dtype=dt)
+            q = m * 2 + s
+            assert np.array_equal(u[q].view(ut), t.view(ut)), (m, s)
+            assert int(out["niter"][q]) == it and int(out["ierr"][q]) == ierr, (m, s, int(out["niter"][q]), it)
