@@ -137,7 +137,7 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 #define MCEIK16_HALOLINE 1       // the fixed instance loads whole halo lines (with the lean words)
 #endif
 #ifndef MCEIK16_NPASS
-#define MCEIK16_NPASS 2          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z)
+#define MCEIK16_NPASS 4          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z; 4 since v39)
 #endif
 #ifndef MCEIK16_NC_SKIP
 #define MCEIK16_NC_SKIP 1        // no nc tests / u0 copies once the iteration is known unconverged (brick16)
