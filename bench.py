@@ -129,22 +129,31 @@ def cpu_baseline(p, v0, cores, rounds=CPU_ROUNDS):
                       f"{float(np.max(times)):.3f} s; proposals/s = cores / median / {p.nstat} stations"}
 
 
+def kfd_devices(nodes):
+    """(physical GPUs, GPU agents) of KFD topology nodes given as property
+    dicts: agents are the nodes with SIMDs; a partitioned MI3xx (CPX / DPX
+    modes) shows each compute partition as its own agent on the same PCI
+    function, so devices are the distinct (domain, location_id) of the agents."""
+    agents = [p for p in nodes if int(p.get("simd_count", 0)) > 0]
+    devs = {(p.get("domain", "0"), p.get("location_id", str(i))) for i, p in enumerate(agents)}
+    return len(devs), len(agents)
+
+
 def node_gpus():
-    """(GPUs of this host, source) from sysfs only (no GPU call): the KFD
-    topology's GPU agents, else the PCI functions of AMD (0x1002) processing
+    """(GPUs of this host, source) from sysfs only (no GPU call): the physical
+    devices of the KFD topology's GPU agents (partitions of one device counted
+    once, `kfd_devices`), else the PCI functions of AMD (0x1002) processing
     accelerators / display controllers (every GPU of the node, whether or not
     this process may use it); (None, None) when neither is readable."""
     base = "/sys/class/kfd/kfd/topology/nodes"
     try:
-        n = 0
+        nodes = []
         for d in os.listdir(base):
             with open(os.path.join(base, d, "properties")) as f:
-                for line in f:
-                    k, _, v = line.partition(" ")
-                    if k == "simd_count" and int(v) > 0:
-                        n += 1
+                nodes.append(dict(line.split(None, 1) for line in f if len(line.split()) == 2))
+        n, agents = kfd_devices([{k: v.strip() for k, v in p.items()} for p in nodes])
         if n:
-            return n, "kfd topology"
+            return n, "kfd topology" + (f" ({agents} partitions)" if agents != n else "")
     except (OSError, ValueError):
         pass
     try:
@@ -199,12 +208,25 @@ def launch_ranks(n):
     return subprocess.call(cmd)
 
 
-def rank_fields(world, steps, per_rank, gather_path=None, gather_check=None, digest_check=None):
+LIB_GATHER = "mceik_mcmc_gather (RCCL)"
+
+
+def gather_path_name(library_comm, rehearse):
+    """The checkpoint gather an N > 1 run times: the library's RCCL gather, or
+    -- when some rank could not build the library communicator (agreed by all
+    ranks) or on the one-GPU rehearsal -- torch.distributed's gather."""
+    if library_comm:
+        return LIB_GATHER
+    return "torch.distributed gather (gloo; one-GPU rehearsal)" if rehearse else "torch.distributed gather (RCCL)"
+
+
+def rank_fields(world, steps, per_rank, gather_path=None, gather_check=None, digest_check=None, comm_error=None):
     """The line's per-rank attribution: `rank_step_ms` {min, max, ranks} (each
     rank's own time per step up to its synchronise), `gather_ms` (the slowest
     rank's checkpoint gather) and, for N > 1, `ranks` and `gather` {path, ms,
-    equals_torch_gather, shards_match_ranks}.  per_rank: [[steps s, gather s]]
-    of every rank."""
+    equals_torch_gather, shards_match_ranks, library_comm}.  per_rank: [[steps
+    s, gather s]] of every rank.  library_comm: "ok", or why the run fell back
+    to torch.distributed's gather."""
     st = [r[0] / steps * 1e3 for r in per_rank]
     out = {"rank_step_ms": {"min": round(min(st), 2), "max": round(max(st), 2), "ranks": len(st)},
            "gather_ms": round(max(r[1] for r in per_rank) * 1e3, 3)}
@@ -214,7 +236,9 @@ def rank_fields(world, steps, per_rank, gather_path=None, gather_check=None, dig
         # (None: no library communicator on this run, torch's gather was the timed path);
         # shards_match_ranks: each rank's block of the gathered posterior = its own kept states
         out["gather"] = {"path": gather_path, "ms": out["gather_ms"], "equals_torch_gather": gather_check,
-                         "shards_match_ranks": digest_check}
+                         "shards_match_ranks": digest_check,
+                         "library_comm": ("ok" if gather_path == LIB_GATHER else
+                                          comm_error or "not built: one-GPU rehearsal (RCCL takes one rank per GPU)")}
     return out
 
 
@@ -417,27 +441,30 @@ def main():
     smp.set_stream(stream.cuda_stream)
 
     comm = post = None
-    gather_path = None
+    gather_path = comm_error = None
     if world > 1:
         # the library's checkpoint gather (mceik_mcmc_gather, RCCL over xGMI);
         # the id travels over the torch.distributed group, as MPI_Bcast would carry it.
-        # If the library cannot build its communicator on this node, every rank
-        # uses torch.distributed's gather instead (same bytes, same collective)
-        # and the line says so.
+        # Decided behaviour when the library cannot build its communicator on
+        # this node: every rank agrees on it BEFORE the collective init
+        # (Comm.from_torch), all ranks gather with torch.distributed instead
+        # (same bytes, RCCL underneath), and the line names the path used and
+        # why (gather.path, gather.library_comm); the run still exits 0.
         ok = 0 if rehearse else 1
         if not rehearse:
             try:
                 comm = mcmc.Comm.from_torch(local_rank)
-            except Exception as exc:          # noqa: BLE001 - reported, not hidden
+            except Exception as exc:          # noqa: BLE001 - reported in the line, not hidden
                 print(f"bench: mceik_comm unavailable ({exc}); gathering with torch.distributed", file=sys.stderr)
+                comm_error = str(exc)
                 ok = 0
         flag = torch.tensor([ok], dtype=torch.int32, device=red_dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if not int(flag.item()) and comm is not None:
             comm.close()
             comm = None
-        gather_path = ("mceik_mcmc_gather (RCCL)" if comm is not None else
-                       "torch.distributed gather (gloo; one-GPU rehearsal)" if rehearse else "torch.distributed gather (RCCL)")
+            comm_error = comm_error or "another rank could not build the communicator"
+        gather_path = gather_path_name(comm is not None, rehearse)
         if rank == 0:
             post = torch.empty((per_gpu * world, p.ncell), dtype=torch.int32, device=dev)
             post_l = torch.empty(per_gpu * world, dtype=torch.float64, device=dev)
@@ -535,7 +562,7 @@ def main():
         }
         if rehearse:
             line["rehearsal"] = "one GPU shared by all ranks (MCEIK_BENCH_REHEARSAL=1): not a scaling measurement"
-        line.update(rank_fields(world, args.steps, per_rank, gather_path, gather_check, digest_check))
+        line.update(rank_fields(world, args.steps, per_rank, gather_path, gather_check, digest_check, comm_error))
         if cpu:
             line["speedup_vs_cpu_per_gpu_share"] = (round(line["value"] / cpu["per_gpu_share_value"], 1)
                                                     if cpu.get("per_gpu_share_value") else None)

@@ -162,6 +162,11 @@ int mceik_mcmc_finalize(mceik_mcmc **s);
  * mpiutils.f90:346-426), then every rank calls mceik_comm_init with its GPU. */
 #define MCEIK_COMM_ID_BYTES 128
 typedef struct mceik_comm mceik_comm;
+/* 1 if this process can build a communicator (RCCL loads and has every entry
+ * point the library uses), else 0.  Local, no GPU call: a launcher agrees on
+ * it over all ranks BEFORE mceik_comm_init, which is collective and would
+ * leave the other ranks waiting for a rank that cannot join. */
+int mceik_comm_available(void);
 int mceik_comm_unique_id(unsigned char id[MCEIK_COMM_ID_BYTES]);
 int mceik_comm_init(const unsigned char id[MCEIK_COMM_ID_BYTES], int nranks, int rank, int device,
                     mceik_comm **out);

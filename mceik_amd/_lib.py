@@ -100,7 +100,7 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_b
            "mceik_mcmc_checkpoint", "mceik_mcmc_restore", "mceik_mcmc_finalize", "mceik_mcmc_last_phase",
            "mceik_mcmc_get_info", "mceik_mcmc_fsm_solves",
            "mceik_parms_defaults", "mceik_parms_set", "mceik_parms_read", "mceik_parms_args", "mceik_parms_write",
-           "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather",
+           "mceik_comm_available", "mceik_comm_unique_id", "mceik_comm_init", "mceik_comm_finalize", "mceik_mcmc_gather",
            "os_path_exists", "os_path_isdir", "os_path_isfile", "os_makedirs", "os_mkdir")
 
 
@@ -174,6 +174,8 @@ def lib():
                                        C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]
     L.mceik_mcmc_fsm_solves.restype = C.c_int
     L.mceik_mcmc_fsm_solves.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    L.mceik_comm_available.restype = C.c_int
+    L.mceik_comm_available.argtypes = []
     L.mceik_comm_unique_id.restype = C.c_int
     L.mceik_comm_unique_id.argtypes = [C.c_void_p]
     L.mceik_comm_init.restype = C.c_int

@@ -74,6 +74,11 @@ struct mceik_comm {
         }                                                                                  \
     } while (0)
 
+extern "C" int mceik_comm_available(void)
+{
+    return mceik_rccl().ok ? 1 : 0;
+}
+
 extern "C" int mceik_comm_unique_id(unsigned char id[MCEIK_COMM_ID_BYTES])
 {
     static_assert(sizeof(ncclUniqueId) == MCEIK_COMM_ID_BYTES, "RCCL id size");

@@ -575,13 +575,39 @@ def gather_kept(smp: Sampler, nchains_total, group=None, dst=0, device=None):
             torch.cat([gl[r][:hi - lo] for r, (lo, hi) in enumerate(parts)]))
 
 
+def comm_ready():
+    """(ok, reason) of this process for the library communicator: the library
+    loads and RCCL has every entry point it uses (mceik_comm_available).  No
+    GPU call."""
+    try:
+        L = _lib.lib()
+    except (OSError, ImportError) as exc:
+        return False, f"libmceik_hip.so: {exc}"
+    if not L.mceik_comm_available():
+        return False, "RCCL (librccl.so.1) cannot be loaded"
+    return True, ""
+
+
+class CommUnavailable(RuntimeError):
+    """Raised on EVERY rank alike when some rank cannot build the communicator
+    (agreed before the collective mceik_comm_init)."""
+
+
 class Comm:
     """RCCL communicator of the library's checkpoint gather (include/mceik.h
     mceik_comm_*): one rank per GPU.  `bootstrap` moves the 128-byte id from
     rank 0 to the others (an MPI main uses MPI_Bcast; here any callable
-    bytes -> bytes, e.g. over torch.distributed: see `from_torch`)."""
+    bytes -> bytes, e.g. over torch.distributed: see `from_torch`).  `agree`
+    (world > 1) maps this rank's `comm_ready()` to every rank's, so that all
+    ranks give up together, before any of them enters the collective
+    mceik_comm_init (which would wait forever for a rank that cannot join)."""
 
-    def __init__(self, rank, world, device, bootstrap=None):
+    def __init__(self, rank, world, device, bootstrap=None, agree=None, ready=comm_ready):
+        if world > 1 and agree is not None:
+            every = agree(ready())
+            bad = [(r, why) for r, (ok, why) in enumerate(every) if not ok]
+            if bad:
+                raise CommUnavailable("; ".join(f"rank {r}: {why}" for r, why in bad))
         L = _lib.lib()
         uid = (C.c_ubyte * 128)()
         mine = None
@@ -598,8 +624,9 @@ class Comm:
         self._h, self._L, self.rank, self.world = h, L, rank, world
 
     @classmethod
-    def from_torch(cls, device, group=None):
-        """Bootstrap over an initialised torch.distributed group."""
+    def from_torch(cls, device, group=None, ready=comm_ready):
+        """Bootstrap (and the readiness agreement) over an initialised
+        torch.distributed group."""
         import torch.distributed as dist
         rank, world = dist.get_rank(group), dist.get_world_size(group)
 
@@ -607,7 +634,12 @@ class Comm:
             box = [b]
             dist.broadcast_object_list(box, src=0, group=group)
             return box[0]
-        return cls(rank, world, device, bcast)
+
+        def agree(mine):
+            every = [None] * world
+            dist.all_gather_object(every, mine, group=group)
+            return every
+        return cls(rank, world, device, bcast, agree, ready)
 
     def gather(self, smp: Sampler, nchains_total, which=1, root=0, v_out=None, logl_out=None):
         """mceik_mcmc_gather: every rank's chains -> `root` in global chain order.

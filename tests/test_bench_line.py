@@ -96,7 +96,7 @@ def test_rank_fields_of_an_n_gt_1_line():
     assert f["rank_step_ms"] == {"min": 2000.0, "max": 2100.0, "ranks": 2}
     assert f["gather_ms"] == 3.0
     assert f["gather"] == {"path": "mceik_mcmc_gather (RCCL)", "ms": 3.0, "equals_torch_gather": True,
-                           "shards_match_ranks": True}
+                           "shards_match_ranks": True, "library_comm": "ok"}
     one = bench.rank_fields(1, 4, [[8.0, 0.001]])
     assert "gather" not in one and one["rank_step_ms"]["ranks"] == 1
 
@@ -125,3 +125,55 @@ def test_cpu_core_share_fields():
         assert c["per_gpu_share_value"] == pytest.approx(0.32 * share / 16, rel=1e-4)
     else:
         assert c["per_gpu_share_cores"] is None and c["per_gpu_share_value"] is None
+
+
+def test_gpus_8_launches_8_distinct_ranks():
+    """C4 readiness (the driver's 8-GPU SCALE run is C4's first execution):
+    `bench.py --gpus 8` starts 8 distinct ranks, LOCAL_RANK 0..7, world 8."""
+    r = _run_bench(["--gpus", "8", "--probe-ranks"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    probes = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"probe"')]
+    assert sorted(q["rank"] for q in probes) == list(range(8)), r.stdout
+    assert sorted(q["local_rank"] for q in probes) == list(range(8))
+    assert all(q["world"] == 8 and q["gpus"] == 8 for q in probes)
+
+
+@pytest.mark.parametrize("total,world", [(8192, 8), (2048, 8), (1024, 2), (1000, 8), (7, 8)])
+def test_shards_tile_the_chains(total, world):
+    """mcmc.shard(total, r, world) over r = 0..world-1 tiles [0, total) in
+    order (C4: 8192 chains = 8 x 1024), sizes differing by at most one."""
+    from mceik_amd import mcmc
+    parts = [mcmc.shard(total, r, world) for r in range(world)]
+    assert parts[0][0] == 0 and parts[-1][1] == total
+    assert all(parts[r][1] == parts[r + 1][0] for r in range(world - 1))
+    sizes = [hi - lo for lo, hi in parts]
+    assert max(sizes) - min(sizes) <= 1
+    if total == 8192:
+        assert parts == [(1024 * r, 1024 * (r + 1)) for r in range(8)]
+
+
+def test_gather_path_is_reported():
+    """Decided N > 1 behaviour without the library communicator: the run
+    gathers with torch.distributed and the line names the path and why."""
+    import bench
+    assert bench.gather_path_name(True, False) == bench.LIB_GATHER
+    assert bench.gather_path_name(False, False) == "torch.distributed gather (RCCL)"
+    assert "rehearsal" in bench.gather_path_name(False, True)
+    ok = bench.rank_fields(8, 2, [[4.0, 0.01]] * 8, bench.LIB_GATHER, True, True)
+    assert ok["ranks"] == 8 and ok["rank_step_ms"]["ranks"] == 8 and ok["gather"]["library_comm"] == "ok"
+    fb = bench.rank_fields(8, 2, [[4.0, 0.01]] * 8, bench.gather_path_name(False, False), None, True,
+                           "rank 3: RCCL (librccl.so.1) cannot be loaded")
+    assert fb["gather"]["path"] == "torch.distributed gather (RCCL)"
+    assert fb["gather"]["library_comm"].startswith("rank 3")
+    assert fb["gather"]["shards_match_ranks"] is True
+
+
+def test_kfd_devices_count_partitions_once():
+    """A CPX-partitioned MI3xx shows several KFD agents on one PCI function:
+    the node's GPU count (for the per-GPU core share) counts the device once."""
+    import bench
+    cpu = {"simd_count": "0", "location_id": "0"}
+    gpu = lambda loc: {"simd_count": "32", "location_id": str(loc), "domain": "0"}
+    assert bench.kfd_devices([cpu] + [gpu(256 * k) for k in range(8)]) == (8, 8)
+    assert bench.kfd_devices([cpu] + [gpu(256 * k) for k in range(8) for _ in range(4)]) == (8, 32)
+    assert bench.kfd_devices([cpu]) == (0, 0)

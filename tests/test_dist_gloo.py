@@ -70,3 +70,44 @@ def test_two_rank_shard_and_gather():
         assert pr.exitcode == 0
     ref, _ = _run_chains(_problem(), 0, nchains, nsteps)
     assert np.array_equal(got, ref)
+
+
+def _comm_worker(rank, world, port, bad_rank, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here); sys.path.insert(0, os.path.dirname(here))
+    import torch.distributed as dist
+    from mceik_amd import mcmc
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+
+    def ready():
+        return (False, "RCCL (librccl.so.1) cannot be loaded") if rank == bad_rank else (True, "")
+    try:
+        mcmc.Comm.from_torch(rank, ready=ready)
+        q.put((rank, "built"))
+    except mcmc.CommUnavailable as exc:
+        q.put((rank, str(exc)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad_rank", [(2, 1), (4, 2)])
+def test_comm_unavailable_on_one_rank_is_agreed_by_all(world, bad_rank):
+    """bench.py's N > 1 gather decision: one rank that cannot build the
+    library communicator makes EVERY rank raise CommUnavailable before the
+    collective mceik_comm_init (no rank is left waiting inside it), each
+    naming the rank and the reason; bench.py then gathers with
+    torch.distributed and reports gather.library_comm."""
+    import torch.multiprocessing as tmp
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, bad_rank, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert sorted(got) == list(range(world))
+    assert all(m == f"rank {bad_rank}: RCCL (librccl.so.1) cannot be loaded" for m in got.values()), got

@@ -40,7 +40,12 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 TOL_REL, TOL_ABS = 4e-6, 4e-7
-BENCH_SIGMA, BENCH_STEPS = 5e-4, 25           # bench.py --sigma default; --warmup 5 + --steps 20 (the driver's run)
+# bench.py's --sigma default; BENCH_STEPS = the driver's round-end bench command (`bench.py --warmup 5
+# --steps 20`, BENCH_r05.json: 20 timed steps of 1643.86 ms), not bench.py's own defaults (--warmup 1 --steps 10)
+BENCH_SIGMA, BENCH_STEPS = 5e-4, 25
+# regression threshold on the observed largest |du| / bound (C3 0.225, C5 0.258 at round 5): the
+# stated bound is 4x the observed maxima; this catches a precision regression of ~2x, not only 4x
+RATIO_REGRESSION = 0.5
 
 
 def _dev():
@@ -138,6 +143,7 @@ def _check_models(p, label, chains, models, dev, sampler_tabs=None, logls=None):
           f"largest |du| / bound {worst_f[3]:.3f} (bound {TOL_REL:g} u + {TOL_ABS:g}); event nodes: "
           f"max |du| {worst_e[0]:.3e} s, max |du|/u {worst_e[1]:.3e}, |du| / bound {worst_e[3]:.3f}")
     assert not fails, fails[:4]
+    assert worst_f[3] <= RATIO_REGRESSION and worst_e[3] <= RATIO_REGRESSION, (worst_f, worst_e)
     return worst_f, worst_e
 
 
@@ -227,11 +233,46 @@ def test_c5_fields_within_fp32_tolerance_of_reference():
         torch.cuda.empty_cache()
     print(f"TOLERANCE C5 fields: max |du|/u {worst[1]:.3e}, largest |du| / bound {worst[3]:.3f}")
     assert not fails, fails
+    assert worst[3] <= RATIO_REGRESSION, worst
 
 
-# identical accept decisions, fp32 vs fp64 sampler: observed 0.99023 (50 of 5120 differ,
-# profiles/r05_a/gpu_tests_tolerance_phases_multistep.log); the floor leaves 2x that fraction of headroom
+# identical accept decisions, fp32 vs fp64 sampler (DESIGN.md s.5): observed at C2 0.99023 (50 of 5120
+# differ, profiles/r05_a/gpu_tests_tolerance_phases_multistep.log); the floor leaves 2x that fraction of
+# headroom.  C3's floor: see test_c3_fp32_and_fp64_samplers_accept_alike.
 ACCEPT_FLOOR = 0.98
+
+
+def _accept_sequences(p, offsets, nch, nsteps, prec):
+    """[step, chain] accept flags of samplers of `nch` chains at each global
+    chain offset (the library's default launch plan), stepped one by one."""
+    from mceik_amd import mcmc
+    out = []
+    for off in offsets:
+        s = mcmc.Sampler(p, nchains=nch, chain_offset=off, precision=prec)
+        seq = []
+        for _ in range(nsteps):
+            s.run(1)
+            seq.append(s.last()[2].astype(bool).copy())
+        s.close()
+        out.append(np.array(seq))
+    return np.concatenate(out, axis=1)
+
+
+def _compare_accepts(label, acc32, acc64, chain_ids):
+    """Prints and returns (identical fraction, chains with identical
+    sequences, first divergence (chain, step))."""
+    same = acc32 == acc64
+    frac = float(same.mean())
+    chains_same = float(same.all(axis=0).mean())
+    bad = np.argwhere(~same)
+    first = None
+    if len(bad):
+        k = int(np.argmin(bad[:, 0] * same.shape[1] + bad[:, 1]))
+        first = (int(chain_ids[bad[k, 1]]), int(bad[k, 0]))     # (global chain, step)
+    print(f"ACCEPT {label} fp32 vs fp64 sampler, {same.shape[1]} chains x {same.shape[0]} steps: identical "
+          f"decisions {frac:.5f} ({int((~same).sum())} differ), chains with identical sequences {chains_same:.4f}, "
+          f"first divergence (chain, step) {first}; accept rate fp32 {acc32.mean():.3f} fp64 {acc64.mean():.3f}")
+    return frac, chains_same, first
 
 
 @pytest.mark.timeout(900)
@@ -243,27 +284,30 @@ def test_c2_fp32_and_fp64_samplers_accept_alike():
     sequence agrees and the first divergent (chain, step); asserts the
     stated floor on identical decisions."""
     _dev()
-    from mceik_amd import mcmc
     p = _bench_problem("C2")
     nch, nsteps = 256, 20
-    acc = {}
-    for prec in (32, 64):
-        s = mcmc.Sampler(p, nchains=nch, precision=prec)
-        seq = []
-        for _ in range(nsteps):
-            s.run(1)
-            seq.append(s.last()[2].astype(bool).copy())
-        acc[prec] = np.array(seq)                            # [step, chain]
-        s.close()
-    same = acc[32] == acc[64]
-    frac = float(same.mean())
-    chains_same = float(same.all(axis=0).mean())
-    bad = np.argwhere(~same)
-    first = None
-    if len(bad):
-        k = int(np.argmin(bad[:, 0] * nch + bad[:, 1]))
-        first = (int(bad[k, 1]), int(bad[k, 0]))           # (chain, step)
-    print(f"ACCEPT C2 fp32 vs fp64 sampler, {nch} chains x {nsteps} steps: identical decisions {frac:.5f} "
-          f"({int((~same).sum())} differ), chains with identical sequences {chains_same:.4f}, first divergence "
-          f"(chain, step) {first}; accept rate fp32 {acc[32].mean():.3f} fp64 {acc[64].mean():.3f}")
+    acc = {prec: _accept_sequences(p, (0,), nch, nsteps, prec) for prec in (32, 64)}
+    frac, _, _ = _compare_accepts("C2", acc[32], acc[64], np.arange(nch))
     assert frac >= ACCEPT_FLOOR
+
+
+# C3 (the headline config): floor stated before the first measurement as C2's (0.98); the measured
+# value is quoted in BASELINE.md beside the headline and in DESIGN.md s.5
+ACCEPT_FLOOR_C3 = 0.98
+
+
+@pytest.mark.timeout(900)
+def test_c3_fp32_and_fp64_samplers_accept_alike():
+    """The same at the headline config C3 (128^3, 32 stations, 32 events, the
+    bench's picks and sigma): 128 chains -- global ids 0..63 and 512..575,
+    i.e. from both halves (pipes) of the bench's 1024-chain sampler -- x the
+    driver's 25 steps, fp32 against
+    fp64 from the same seed.  Chains are keyed by global id, so these are
+    the bench's own chains' decisions."""
+    _dev()
+    p = _bench_problem("C3")
+    offsets, nch, nsteps = (0, 512), 64, BENCH_STEPS
+    ids = np.concatenate([np.arange(o, o + nch) for o in offsets])
+    acc = {prec: _accept_sequences(p, offsets, nch, nsteps, prec) for prec in (32, 64)}
+    frac, chains_same, first = _compare_accepts("C3", acc[32], acc[64], ids)
+    assert frac >= ACCEPT_FLOOR_C3
