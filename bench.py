@@ -252,11 +252,12 @@ def shard_digest(v, logl):
 
 
 # ---------------------------------------------------------------- roofline
-def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config, kname=None):
+def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config, kname=None, multi_step=False):
     """The `roofline` object of a timed region: algorithmic bytes of the FSM
     launches (visited bricks x nodes x bytes per node sweep)
     over the FSM time of a step -- the HIP-event launch duration with one
-    pipe, the wall time per step with overlapped pipes."""
+    pipe, the wall time per step with overlapped pipes or with multi-step
+    launches (several steps per launch, mceik_mcmc_get_info.multi_step)."""
     fsm_ms, nlaunch, iters, (bricks, segs, segs_changed, wsteps) = stats
     n_nodes = p.nx * p.ny * p.nz
     from mceik_amd import _lib
@@ -279,8 +280,9 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config, kname=None):
     solves_per_step = per_gpu * p.nstat                 # this rank's (chain, station) solves
     alg_step = alg_bytes / steps                        # algorithmic bytes of one step (all pipes)
     achieved = per_launch = alg_bytes / max(nlaunch, 1) / (avg_ms * 1e-3) / 1e9
-    pipes = round(nlaunch / steps)                      # 1 if the sampler fell back to one pipe
-    if pipes > 1:
+    pipes = 1 if multi_step else round(nlaunch / steps)  # 1 if the sampler fell back to one pipe
+    wall = pipes > 1 or multi_step
+    if wall:
         # two half launches per step, overlapped: a half's HIP-event span also
         # covers the time it waits for the other half's waves, so price one
         # step's algorithmic bytes on the step's wall time instead (includes
@@ -288,7 +290,7 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config, kname=None):
         achieved = alg_bytes / elapsed / 1e9                  # this rank's bytes, the timed region
     # the FSM time of one step: the single launch (HIP events) or, with pipes,
     # the wall time per step (the overlapped half launches' union is shorter)
-    step_fsm_s = avg_ms * 1e-3 if pipes <= 1 else elapsed / steps
+    step_fsm_s = elapsed / steps if wall else avg_ms * 1e-3
     traffic = traffic_src = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf):
@@ -304,7 +306,8 @@ def roofline(p, per_gpu, precision, stats, elapsed, nsteps, config, kname=None):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": kname,
             "kernel_rev": KERNEL_REVS[precision],
-            "timing": (f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
+            "timing": ("wall time per step (multi-step launches: several steps per launch)" if multi_step else
+                       f"wall time per step ({pipes} overlapped partial launches, MCEIK_PIPES={pipes})"
                        if pipes > 1 else "HIP events around each FSM launch"),
             "per": "step: every per-unit field below is per step or per solve, whatever the pipes",
             "pipes": pipes,
@@ -344,7 +347,8 @@ def f64_record(p, v0, per_gpu, args, dev, stream):
     stats = smp.fsm_stats()
     info = smp.info()
     smp.close()
-    rl = roofline(p, per_gpu, 64, stats, elapsed, args.f64_steps, args.config, kname=info["kernel"])
+    rl = roofline(p, per_gpu, 64, stats, elapsed, args.f64_steps, args.config, kname=info["kernel"],
+                  multi_step=info["multi_step"])
     rl["lds_bytes_per_wave"] = info["lds_bytes"]
     return {"value": round(per_gpu * args.f64_steps / elapsed, 3), "unit": "proposals/s", "dtype": "f64",
             "steps": args.f64_steps, "warmup": args.f64_warmup,
@@ -535,7 +539,8 @@ def main():
 
     if rank == 0:
         total = per_gpu * world * args.steps
-        rl = roofline(p, per_gpu, args.precision, stats, elapsed, args.steps, args.config, kname=info["kernel"])
+        rl = roofline(p, per_gpu, args.precision, stats, elapsed, args.steps, args.config, kname=info["kernel"],
+                      multi_step=info["multi_step"])
         rl["lds_bytes_per_wave"] = info["lds_bytes"]
         line = {
             "metric": METRIC,

@@ -177,3 +177,19 @@ def test_kfd_devices_count_partitions_once():
     assert bench.kfd_devices([cpu] + [gpu(256 * k) for k in range(8)]) == (8, 8)
     assert bench.kfd_devices([cpu] + [gpu(256 * k) for k in range(8) for _ in range(4)]) == (8, 32)
     assert bench.kfd_devices([cpu]) == (0, 0)
+
+
+def test_roofline_of_multi_step_launches():
+    """A multi-step sampler (several steps per launch, e.g. 32 chains per
+    rank in the 8-rank rehearsal: 0.5 launches per step) reports one pipe and
+    prices a step's bytes on the wall time per step (round 6: it printed
+    pipes 0 and the per-launch time as the step's)."""
+    import bench
+    from mceik_amd import mcmc
+    p = mcmc.make_problem("C3", picks="analytic")
+    stats = (2000.0, 1, 32 * 32 * 6 * 2, (1.0e8, 3.0e9, 1.0e9, 1.0e7))
+    r = bench.roofline(p, 32, 32, stats, 1.5, 2, "C3", multi_step=True)
+    assert r["pipes"] == 1 and r["launches_per_step"] == 0.5
+    assert r["fsm_s_per_step"] == pytest.approx(0.75)
+    assert r["achieved"] == pytest.approx(1.0e8 * 512 * r["bytes_per_node_sweep"] / 1.5 / 1e9, rel=1e-3)
+    assert r["timing"].startswith("wall time per step (multi-step")
