@@ -2370,15 +2370,9 @@ extern "C" int mceik_mcmc_fsm_stats(mceik_mcmc *s, double *fsm_ms, long long *nl
         unsigned long long tsum = 0;
         for (int k = 0; k < MCEIK_TRAFFIC_N; k++) tsum += it[6 + k];
         if (tsum && s->nlaunch) {
-#ifdef MCEIK_ADMIT_STATS
-            static const char *nm[MCEIK_TRAFFIC_N] = {"self", "neighbour", "inflight", "run", "self_chg",
-                                                      "neighbour_chg", "inflight_chg", "run_chg"};
-            fprintf(stderr, "mceik admissions (z-block visits by reason per FSM launch, %lld launches):", s->nlaunch);
-#else
             static const char *nm[MCEIK_TRAFFIC_N] = {"own_load", "halo_load", "zup_load", "own_store",
                                                       "u0_store", "cell_load", "verify_load", "init_gather"};
             fprintf(stderr, "mceik traffic (requested bytes per FSM launch, %lld launches):", s->nlaunch);
-#endif
             for (int k = 0; k < MCEIK_TRAFFIC_N; k++) fprintf(stderr, " %s=%.6e", nm[k], (double)it[6 + k] / s->nlaunch);
             fprintf(stderr, " total=%.6e\n", (double)tsum / s->nlaunch);
         }

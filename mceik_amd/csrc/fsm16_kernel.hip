@@ -127,25 +127,13 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
     lds_w4(x + XROW16(arr, 2 * h + 1, row), v[4], v[5], v[6], v[7]);
 }
 
-#ifndef MCEIK16_FULLLINE
-#define MCEIK16_FULLLINE 1       // the fixed instance (2-step positions) loads whole own lines
-#endif
-#ifndef MCEIK16_LEAN
-#define MCEIK16_LEAN 1           // the fixed instance decodes lean position words
-#endif
-#ifndef MCEIK16_HALOLINE
-#define MCEIK16_HALOLINE 1       // the fixed instance loads whole halo lines (with the lean words)
-#endif
-#ifndef MCEIK16_NPASS
-#define MCEIK16_NPASS 4          // neighbour-row passes per 16-z brick update (2: 8 z, 4: 4 z; 4 since v39)
-#endif
-#ifndef MCEIK16_NC_SKIP
-#define MCEIK16_NC_SKIP 1        // no nc tests / u0 copies once the iteration is known unconverged (brick16)
-#endif
-#ifndef MCEIK16_HOLD
-#define MCEIK16_HOLD 1           // the held stream (fsm_hold.h): face-level change marks, blocks with an
-                                 // in-flight dependency and no settled reason wait instead of being visited
-#endif
+// The fixed instance (2-step positions) loads whole own lines (FL), decodes
+// lean position words (LEAN) and loads whole halo lines (HFL); every instance
+// runs the held stream (fsm_hold.h: face-level change marks, blocks with an
+// in-flight dependency and no settled reason wait instead of being visited).
+// The brick update reads its neighbour rows in four passes of 4 z (v39: half
+// the neighbour registers of two 8-z passes).
+#define NPASS16 4
 // BInfo16.w1 bit 24: the brick is the last of its position below the column end, so its z-downwind
 // node is loaded from HBM (into the z-boundary register with the run-start node) for a run that
 // does not continue
@@ -158,24 +146,10 @@ __device__ __forceinline__ void halo_stage16(float *x, int lane, const float (&v
 //   i1: even own q2,     odd partner's q3     (even's line)
 //   i2: even partner q0, odd own q1           (odd's line)
 //   i3: even partner q2, odd own q3           (odd's line)
-// even then holds E0 E2 O0 O2 and odd E1 E3 O1 O3; seg_finish swaps the
-// partner's quarters (DPP quad_perm [1,0,3,2]).
-// MCEIK16_PAIR = 0: every lane loads / stores its own four quarters (each
-// instruction touches 64 lines; no swap VALU)
-#ifndef MCEIK16_PAIR
-#define MCEIK16_PAIR 1
-#endif
+// even then holds E0 E2 O0 O2 and odd E1 E3 O1 O3, written straight into
+// the neighbour rows they belong to (raw_write below).
 __device__ __forceinline__ void seg_issue(Rsrc r, uint32_t seg, float (&a)[16])
 {
-    if (!MCEIK16_PAIR) {
-        float t[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            bload4(r, seg + 16u * q, t);
-            a[4 * q] = t[0]; a[4 * q + 1] = t[1]; a[4 * q + 2] = t[2]; a[4 * q + 3] = t[3];
-        }
-        return;
-    }
     const bool odd = threadIdx.x & 1;
     const uint32_t segp = dpp_swap_pair(seg);
     float t[4];
@@ -187,26 +161,6 @@ __device__ __forceinline__ void seg_issue(Rsrc r, uint32_t seg, float (&a)[16])
     a[8] = t[0]; a[9] = t[1]; a[10] = t[2]; a[11] = t[3];
     bload4(r, odd ? seg + 48u : segp + 32u, t);
     a[12] = t[0]; a[13] = t[1]; a[14] = t[2]; a[15] = t[3];
-}
-__device__ __forceinline__ void seg_finish(const float (&a)[16], float (&v)[16])
-{
-    if (!MCEIK16_PAIR) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) v[i] = a[i];
-        return;
-    }
-    const bool odd = threadIdx.x & 1;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        // even sends its O0 O2 (a[8..15]), odd its E1 E3 (a[0..7])
-        const float send = odd ? a[i] : a[8 + i];
-        const float recv = __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(unsigned, send)));
-        const int q = i >> 2, k = i & 3;       // q = 0: quarter 0/1 pair, q = 1: quarter 2/3 pair
-        // even: own quarters 0 and 2 = a[4q + k] (i0, i1), received 1 and 3
-        // odd:  own quarters 1 and 3 = a[8 + 4q + k] (i2, i3), received 0 and 2
-        v[8 * q + k] = odd ? recv : a[4 * q + k];
-        v[8 * q + 4 + k] = odd ? a[8 + 4 * q + k] : recv;
-    }
 }
 // The pair exchange through the neighbour rows instead of DPP swaps (no
 // VALU): the raw quarters of seg_issue are written straight into the rows
@@ -300,35 +254,6 @@ __device__ __forceinline__ void raw_store(Rsrc r, uint32_t seg, bool chg, const 
     bstore4(r, b23, t[8], t[9], t[10], t[11]);
     bstore4(r, b23 + 32u, t[12], t[13], t[14], t[15]);
 }
-// changed segments only: the same pairing for the write-back
-__device__ __forceinline__ void seg_store(Rsrc r, uint32_t seg, bool chg, const float (&v)[16])
-{
-    if (!MCEIK16_PAIR) {
-        const uint32_t own = chg ? seg : OOB;
-#pragma unroll
-        for (int q = 0; q < 4; q++) bstore4(r, own + 16u * q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-        return;
-    }
-    const bool odd = threadIdx.x & 1;
-    const uint32_t own = chg ? seg : OOB;
-    const uint32_t oth = dpp_swap_pair(own);
-    float x[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        // even sends its quarters 1, 3; odd its quarters 0, 2
-        const int q = i >> 2, k = i & 3;
-        const float send = odd ? v[8 * q + k] : v[8 * q + 4 + k];
-        x[i] = __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(unsigned, send)));
-    }
-    // i0: even own q0 | odd partner's q1 (x = even's q1)      i1: even own q2 | odd partner's q3
-    // i2: even partner's q0 (x = odd's q0) | odd own q1        i3: even partner's q2 | odd own q3
-    bstore4(r, odd ? oth + 16u : own, odd ? x[0] : v[0], odd ? x[1] : v[1], odd ? x[2] : v[2], odd ? x[3] : v[3]);
-    bstore4(r, odd ? oth + 48u : own + 32u, odd ? x[4] : v[8], odd ? x[5] : v[9], odd ? x[6] : v[10],
-            odd ? x[7] : v[11]);
-    bstore4(r, odd ? own + 16u : oth, odd ? v[4] : x[0], odd ? v[5] : x[1], odd ? v[6] : x[2], odd ? v[7] : x[3]);
-    bstore4(r, odd ? own + 48u : oth + 32u, odd ? v[12] : x[4], odd ? v[13] : x[5], odd ? v[14] : x[6],
-            odd ? v[15] : x[7]);
-}
 __device__ __forceinline__ void store16_plain(Rsrc r, uint32_t off, const float (&v)[16])
 {
 #pragma unroll
@@ -336,12 +261,9 @@ __device__ __forceinline__ void store16_plain(Rsrc r, uint32_t off, const float 
 }
 
 // ---- brick / halo addressing ------------------------------------------------
-#ifndef MCEIK_HALO_AUX
-#define MCEIK_HALO_AUX MCEIK_LD_AUX
-#endif
 __device__ __forceinline__ void bload4h(Rsrc r, uint32_t off, float (&v)[4])
 {
-    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MCEIK_HALO_AUX));
+    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 // Brick info of one lane's brick, packed (b0 / b1 ride two steps in VGPRs):
@@ -380,8 +302,8 @@ __device__ __forceinline__ BInfo16 brick_info16(const FsmLaunch &L, const Fsm16G
     if (zb == (RZ ? 0 : g.nzb - 1)) fl |= F_LAST;
     // held stream: the z-boundary nodes come from the z-face copies (zf), the run end's z-downwind
     // node of the position's last brick below the column end included
-    const bool zd = MCEIK16_HOLD && valid && p.zbs == kb - 1 && !(fl & F_LAST);
-    if (MCEIK16_HOLD && b.zh != OOB) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], false, lx, ly);
+    const bool zd = valid && p.zbs == kb - 1 && !(fl & F_LAST);
+    if (b.zh != OOB) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], false, lx, ly);
     if (zd) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], true, lx, ly);
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
     bool slow = (fl & C_PART) || ((fl & C_00) && zb == 0) || (valid && zb * 16 + 16 > L.nz);
@@ -468,8 +390,8 @@ __device__ __forceinline__ BInfo16 brick_info_lean(const FsmLaunch &L, const Sme
     b.zh = valid && (gp & 8u) ? off + (RZ ? 8192u - 64u : 124u - 8192u) : OOB;
     // held stream: the z-boundary nodes come from the z-face copies (zf), the run end's z-downwind
     // node of the position's last brick below the column end included
-    const bool zd = MCEIK16_HOLD && valid && ph == 1 && !(gp & 2u);
-    if (MCEIK16_HOLD && b.zh != OOB) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], false, lx, ly);
+    const bool zd = valid && ph == 1 && !(gp & 2u);
+    if (b.zh != OOB) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], false, lx, ly);
     if (zd) b.zh = zf_boundary<float, RZ>(L, S.ring_b[p.ri], true, lx, ly);
     int fl = valid ? (int)((w & 0x7fu) | F_VALID | ((gp & 15u) << 8)) : 0;
     unsigned bcm = 0;
@@ -555,79 +477,6 @@ __device__ __forceinline__ void build_order16(const FsmLaunch &L, unsigned short
     }
 }
 
-// ---- stream decisions (as decide() in fsm_kernel.hip, 16-bit clocks) -----
-template <bool RZ>
-__device__ __forceinline__ int decide16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, Stream &st, int C,
-                                        int rx, int ry, int &zh)
-{
-    const int lane = threadIdx.x;
-    const int nt = L.ntiles, nzk = L.nzk;
-    zh = 0;
-    if (st.tile < 0) {
-        while (st.cursor < nt) {
-            const int k = st.cursor + lane;
-            int k0 = nzk, entry = 0;
-            if (k < nt) {
-                const int o = S.order[k];
-                const int txs = o & 0xff, tys = o >> 8;
-                const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
-                const int id = ty * L.ntx + tx;
-                const int xu = txs > 0 ? id + (rx ? 1 : -1) : -1;
-                const int yu = tys > 0 ? id + (ry ? L.ntx : -L.ntx) : -1;
-                entry = tx | (ty << 12);
-                for (int kz = 0; kz < nzk; kz++) {
-                    const int tz = RZ ? nzk - 1 - kz : kz;
-                    const int b = tz * nt + id;
-                    const int lp = S.lastproc[b];
-                    bool d = S.lastchg[b] >= lp;
-                    if (tx > 0) d |= S.lastchg[b - 1] > lp;
-                    if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
-                    if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
-                    if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
-                    if (tz > 0) d |= S.lastchg[b - nt] > lp;
-                    if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
-                    if (xu >= 0) d |= (int)S.lastproc[tz * nt + xu] > C - g.infl;
-                    if (yu >= 0) d |= (int)S.lastproc[tz * nt + yu] > C - g.infl;
-                    if (d) { k0 = kz; break; }
-                }
-            }
-            const unsigned long long m = __ballot(k0 < nzk);
-            if (m) {
-                const int first = __builtin_ctzll(m);
-                st.cursor += first + 1;
-                st.tile = __builtin_amdgcn_readfirstlane(__shfl(entry, first, 64));
-                st.k0 = st.k = __builtin_amdgcn_readfirstlane(__shfl(k0, first, 64));
-                break;
-            }
-            st.cursor += 64;
-        }
-        if (st.tile < 0) return -2;
-        // bubbles before the run: block k sits at position pos + wait + (k - k0),
-        // which must be >= vis positions after its upwind x/y neighbours' visits
-        const int tx = st.tile & 0xfff, ty = st.tile >> 12;
-        const int txs = rx ? L.ntx - 1 - tx : tx, tys = ry ? L.nty - 1 - ty : ty;
-        const int id = ty * L.ntx + tx;
-        int need = 0;
-        for (int kz = st.k0 + lane; kz < nzk; kz += 64) {
-            const int tz = RZ ? nzk - 1 - kz : kz;
-            int p = -0x40000000;
-            if (txs > 0) p = max(p, (int)S.lastproc[tz * nt + id + (rx ? 1 : -1)]);
-            if (tys > 0) p = max(p, (int)S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)]);
-            need = max(need, p + g.vis - (kz - st.k0) - C);
-        }
-        st.wait = __builtin_amdgcn_readfirstlane(wave_max(need));
-    }
-    if (st.wait > 0) {
-        st.wait--;
-        return -1;
-    }
-    const int kz = st.k;
-    zh = kz == st.k0 && kz > 0;
-    const int tz = RZ ? nzk - 1 - kz : kz;
-    const int e = st.tile | (tz << 24);
-    if (++st.k == nzk) st.tile = -1;
-    return e;
-}
 
 // the held stream's LDS arrays (fsm_hold.h)
 __device__ __forceinline__ HoldLds<unsigned short> hold_lds16(const Smem16 &S)
@@ -638,75 +487,11 @@ __device__ __forceinline__ HoldLds<unsigned short> hold_lds16(const Smem16 &S)
     return H;
 }
 
-#ifdef MCEIK_ADMIT_STATS
-// Experiment build (-DMCEIK_TRAFFIC -DMCEIK_ADMIT_STATS; the traffic
-// counters then hold admission statistics instead of bytes): why each
-// admitted z-block was visited -- 1 it changed at its last visit, 2 a face
-// neighbour changed since, 3 only its upwind x/y neighbour is in flight,
-// 4 none of these (the continuation of a z-run) -- counted in [reason - 1],
-// and in [3 + reason] when the visit changed the block.  A slot's previous
-// position is settled when the slot is reused (nr positions later: every
-// lane is past it) or at the end of the sweep (admit_flush16).
-__device__ __forceinline__ void admit_settle16(const Smem16 &S, int ri)
-{
-    const int r = S.scratch[16 + ri];
-    if (r) {
-        const int b = S.ring_b[ri];
-        S.scratch[8 + r - 1] += 1;
-        if (S.lastchg[b] == S.lastproc[b]) S.scratch[8 + 3 + r] += 1;
-        S.scratch[16 + ri] = 0;
-    }
-}
-__device__ __forceinline__ void admit_account16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, int entry,
-                                                int ri, int C, int rx, int ry)
-{
-    asm volatile("" ::: "memory");
-    if (threadIdx.x == 0) {
-        admit_settle16(S, ri);
-        if (entry >= 0) {
-            const int nt = L.ntiles;
-            const int tz = (entry >> 24) & 0xff, tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
-            const int id = ty * L.ntx + tx, b = tz * nt + id;
-            const int txs = rx ? L.ntx - 1 - tx : tx, tys = ry ? L.nty - 1 - ty : ty;
-            const int lp = S.lastproc[b];
-            int r = 4;
-            if (S.lastchg[b] >= lp) {
-                r = 1;
-            } else {
-                bool d = false;
-                if (tx > 0) d |= S.lastchg[b - 1] > lp;
-                if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
-                if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
-                if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
-                if (tz > 0) d |= S.lastchg[b - nt] > lp;
-                if (tz < L.nzk - 1) d |= S.lastchg[b + nt] > lp;
-                if (d) {
-                    r = 2;
-                } else {
-                    bool f = false;
-                    if (txs > 0) f |= (int)S.lastproc[tz * nt + id + (rx ? 1 : -1)] > C - g.infl;
-                    if (tys > 0) f |= (int)S.lastproc[tz * nt + id + (ry ? L.ntx : -L.ntx)] > C - g.infl;
-                    if (f) r = 3;
-                }
-            }
-            S.scratch[16 + ri] = r;
-        }
-    }
-    asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void admit_flush16(const Smem16 &S, int nr)
-{
-    asm volatile("" ::: "memory");
-    if (threadIdx.x == 0)
-        for (int ri = 0; ri < nr; ri++) admit_settle16(S, ri);
-    asm volatile("" ::: "memory");
-}
-#endif
 
 // Admit position (ring slot ri, relative clock C): every lane writes its
 // column meta, lane 0 the ring entry, block id, tile base and the block's
-// visit clock.  u0 flag: the block's first visit in this iteration
-// (lastproc is rebased to 1 at every iteration start, iter_norm()).
+// visit clock.  u0 flag: the block's first visit in this iteration (the
+// held stream's visited bitmap).
 template <bool RZ, bool LEAN>
 __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, const BcBoxes &bc,
                                         int entry, int zh, int ri, int C, int lx, int ly, int lxs, int lys, int rx,
@@ -715,16 +500,13 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
     unsigned meta = 0;
     int bid = 0, nbv = 0;
     uint32_t base = 0;
-#if defined(MCEIK_ADMIT_STATS) && !MCEIK16_HOLD
-    admit_account16(L, g, S, entry, ri, C, rx, ry);
-#endif
     if (entry >= 0) {
         const int tz = (entry >> 24) & 0xff, tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
         bid = tz * L.ntiles + tx + ty * L.ntx;
         nbv = min(L.kb, L.nzb - tz * L.kb);          // 8-z bricks of the block (visit statistics)
-        // no visit since the iteration started (clock 64; the held stream's clocks restart every
-        // sweep, so there the iteration's visits are a bitmap)
-        const int u0flag = MCEIK16_HOLD ? !((S.vbits[bid >> 5] >> (bid & 31)) & 1u) : S.lastproc[bid] < 64;
+        // no visit since the iteration started (the held stream's clocks restart every sweep, so the
+        // iteration's visits are a bitmap)
+        const int u0flag = !((S.vbits[bid >> 5] >> (bid & 31)) & 1u);
         if ((entry & 0xffffff) != ct.tile) column_tile<float>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         meta = LEAN ? lean_word<RZ>(L, g, ct, tz, ri, u0flag, zh) : column_word(L, L.kb, ct, tz, ri, u0flag, zh);
         base = (uint32_t)(ty * L.ntx + tx) * tile_bytes<float>(L) + (LEAN ? (uint32_t)tz << 13 : 0u);
@@ -735,7 +517,7 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
     if (threadIdx.x == 0) {
         if (entry >= 0) {
             S.lastproc[bid] = (unsigned short)C;
-            if (MCEIK16_HOLD) S.vbits[bid >> 5] |= 1u << (bid & 31);
+            S.vbits[bid >> 5] |= 1u << (bid & 31);
             if (L.visit_stats) {
                 S.scratch[0] += nbv;
                 S.scratch[1] += nbv * nact;
@@ -748,39 +530,6 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
     asm volatile("" ::: "memory");
 }
 
-// Start of an iteration: every block's pending state (it changed at its last
-// visit, or a face neighbour changed since) becomes lastchg 1 / 0 against
-// lastproc 1, and the clock restarts at 64.  The decisions of the iteration
-// are those of unbounded clocks (all that matters of the past is the
-// pending state; nothing is in flight across an iteration boundary), and an
-// iteration needs at most 8 (nblocks (1 + vis) + infl) + 64 < 2^16 clocks.
-__device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
-{
-    const int nt = L.ntiles, nzk = L.nzk;
-    unsigned pend = 0;                       // bit i: block lane + 64 i (nblocks <= 1024)
-    for (int i = 0; i * 64 < L.nblocks; i++) {
-        const int b = threadIdx.x + 64 * i;
-        if (b >= L.nblocks) break;
-        const int tz = b / nt, id = b - tz * nt, ty = id / L.ntx, tx = id - ty * L.ntx;
-        const int lp = S.lastproc[b];
-        bool d = S.lastchg[b] >= lp;
-        if (tx > 0) d |= S.lastchg[b - 1] > lp;
-        if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
-        if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
-        if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
-        if (tz > 0) d |= S.lastchg[b - nt] > lp;
-        if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
-        if (d) pend |= 1u << i;
-    }
-    asm volatile("" ::: "memory");
-    for (int i = 0; i * 64 < L.nblocks; i++) {
-        const int b = threadIdx.x + 64 * i;
-        if (b >= L.nblocks) break;
-        S.lastproc[b] = 1;
-        S.lastchg[b] = (pend >> i) & 1u;
-    }
-    asm volatile("" ::: "memory");
-}
 
 // The 16 z-slots of the current brick, updated in place (v).  GENERIC as in
 // fsm_kernel.hip brick_update (grid-edge columns of cut tiles, cut z-bricks,
@@ -789,7 +538,7 @@ __device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem16 &S)
 // NC: evaluate the "changed while >= T" test (nc).  Once a lane of the wave
 // has found the iteration unconverged, the test cannot change the outcome
 // (the iteration runs again, its verify and u0 copies are not used), so the
-// sweep drops it for the rest of the iteration (MCEIK16_NC_SKIP).
+// sweep drops it for the rest of the iteration.
 template <bool RZ, bool GENERIC, bool LEAN, bool NC = true>
 __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, const BInfo16 &b0, float (&v)[16],
                                         float zprev0, float znext, int lx, int ly, int rx, int ry, bool &changed,
@@ -814,24 +563,16 @@ __device__ __forceinline__ void brick16(const FsmLaunch &L, const Smem16 &S, con
     const int rxp = lxs < 7 ? lane + 1 : 64 + lys, ryp = lys < 7 ? lane + 8 : 72 + lxs;
     float fc = 0.f, ffc = 0.f, ff2c = 0.f, ff3c = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < MCEIK16_NPASS; hh++) {
-        // the part of the brick this pass updates (sweep order: low z first
-        // unless RZ) and the four neighbour rows' values for it: halves (8 z,
-        // MCEIK16_NPASS 2) or quarters (4 z, 4: half the neighbour registers)
-        constexpr int PZ = 16 / MCEIK16_NPASS;
-        const int h = RZ ? MCEIK16_NPASS - 1 - hh : hh;
+    for (int hh = 0; hh < NPASS16; hh++) {
+        // the quarter of the brick this pass updates (4 z; sweep order: low z
+        // first unless RZ) and the four neighbour rows' values for it
+        constexpr int PZ = 16 / NPASS16;
+        const int h = RZ ? NPASS16 - 1 - hh : hh;
         float xm[PZ], xq[PZ], ym[PZ], yq[PZ];
-        if (PZ == 8) {
-            load_half16(S.xr, 0, rxm, h, *reinterpret_cast<float (*)[8]>(&xm[0]));
-            load_half16(S.xr, 0, rym, h, *reinterpret_cast<float (*)[8]>(&ym[0]));
-            load_half16(S.xr, 1, rxp, h, *reinterpret_cast<float (*)[8]>(&xq[0]));
-            load_half16(S.xr, 1, ryp, h, *reinterpret_cast<float (*)[8]>(&yq[0]));
-        } else {
-            lds_r4(S.xr + XROW16(0, h, rxm), xm[0], xm[1], xm[2], xm[3]);
-            lds_r4(S.xr + XROW16(0, h, rym), ym[0], ym[1], ym[2], ym[3]);
-            lds_r4(S.xr + XROW16(1, h, rxp), xq[0], xq[1], xq[2], xq[3]);
-            lds_r4(S.xr + XROW16(1, h, ryp), yq[0], yq[1], yq[2], yq[3]);
-        }
+        lds_r4(S.xr + XROW16(0, h, rxm), xm[0], xm[1], xm[2], xm[3]);
+        lds_r4(S.xr + XROW16(0, h, rym), ym[0], ym[1], ym[2], ym[3]);
+        lds_r4(S.xr + XROW16(1, h, rxp), xq[0], xq[1], xq[2], xq[3]);
+        lds_r4(S.xr + XROW16(1, h, ryp), yq[0], yq[1], yq[2], yq[3]);
 #pragma unroll
         for (int jj = 0; jj < PZ; jj++) {
             const int j = hh * PZ + jj;                     // sweep-order slot
@@ -895,7 +636,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
                                        const BcBoxes &bc, const Smem16 &S, int rx, int ry, int clock0, bool &notconv,
                                        int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
-    const Rsrc zr_ = MCEIK16_HOLD ? zfr : ur;        // where the z-boundary nodes are read
+    const Rsrc zr_ = zfr;                            // the z-boundary nodes: the z-face copies
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const float UN = FLT_MAX;
@@ -910,9 +651,6 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     const int hlx = rx ? 7 - (he & 7) : (he & 7), hly = ry ? 7 - (he >> 3) : (he >> 3);
     const uint32_t hcol = (uint32_t)colpos(hlx, hly) * 128u;
 
-    Stream st;
-    st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
-    constexpr bool HOLD = MCEIK16_HOLD;
     const HoldLds<unsigned short> H = hold_lds16(S);
     // (the held stream's scan state -- first incomplete tile, previous position's tile -- lives in LDS
     // scratch [4], [5]: fewer scalar registers live across the step loop)
@@ -920,22 +658,19 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     // lane's column is a tile edge (absolute orientation)
     const unsigned xyface = HOLD_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
                             (ly == 7 ? 16u : 0u);
-    if (HOLD) {
-        hold_norm(L, H);
-        if (lane == 0) { S.scratch[4] = 0; S.scratch[5] = -1; }
-        clock0 = 64;
-    }
-    // the next position's block (held stream: after settling the visit infl positions back)
+    hold_norm(L, H);
+    if (lane == 0) { S.scratch[4] = 0; S.scratch[5] = -1; }
+    clock0 = 64;
+    // the next position's block (after settling the visit infl positions back)
     auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
-        if (!HOLD) return decide16<RZ>(L, g, S, st, clock0 + pos, rx, ry, zh);
         // positions are decided one after another: settle the one infl back
         const int q = pos - g.infl;
         if (q >= 0) hold_settle(L, H, q % nr, clock0 + q);
         return hold_decide<RZ>(L, H, S.scratch + 4, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, g.infl, g.vis,
                                zh);
     };
-    constexpr bool FL = KB16 == 2 && MCEIK16_FULLLINE;   // full-line own loads (2-step positions)
-    constexpr bool LEAN = KB16 == 2 && MCEIK16_LEAN;     // lean position words (2-step positions)
+    constexpr bool FL = KB16 == 2;                   // full-line own loads (2-step positions)
+    constexpr bool LEAN = KB16 == 2;                 // lean position words (2-step positions)
     // ping-pong register sets by step parity (the step loop runs in pairs, so
     // no register copies at the loop latch): halo values hs[p] loaded at the
     // step before, staged at the end of step p, hs[1 - p] loading; FL's held
@@ -949,7 +684,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     // hA[P]: the first brick loaded at a step of parity P, staged at the end
     // of the next step; hB[P]: the second brick, staged two steps later (hBs
     // holds it over the step that reloads hB[P])
-    constexpr bool HFL = FL && LEAN && MCEIK16_HALOLINE;
+    constexpr bool HFL = FL && LEAN;
     const int hr = lane & 3, hpi = (lane >> 4) & 1, hcme = (lane >> 1) & 1;
     const int hj0 = (lane >> 1) & ~1;
     const int hst = XROW16((hj0 >> 3) & 1, hr, 64 + ((hj0 >> 4) << 3) + (hj0 & 7));   // column 2i's row, quarter r
@@ -991,12 +726,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     {
         float t[16];
         seg_issue(ur, b0.seg, t);
-        if (MCEIK16_PAIR) {                           // through this lane's XN row
-            raw_write(S.xr, pbn, t);
-            load_row16(S.xr, 1, lane, v);
-        } else {
-            seg_finish(t, v);
-        }
+        raw_write(S.xr, pbn, t);                      // through this lane's XN row
+        load_row16(S.xr, 1, lane, v);
     }
     pos_init(pe, -hd, kb, nr);
     {
@@ -1015,13 +746,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     {
         float t[16];
         seg_issue(ur, b1.seg, t);
-        if (MCEIK16_PAIR) {
-            raw_write(S.xr, pbn, t);                    // brick vb0 + 1: the XN rows
-        } else {
-            float n[16];
-            seg_finish(t, n);
-            store_row16(S.xr, 1, lane, n);
-        }
+        raw_write(S.xr, pbn, t);                        // brick vb0 + 1: the XN rows
     }
     if (FL) {
         // the held half for step 0: the lane whose step-0 target is the second
@@ -1165,7 +890,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         }
         // ---- u0: old values of a block's first visit in the iteration (< T only); none once the
         // iteration is known unconverged (the verify that reads them does not run)
-        const bool wnc = !MCEIK16_NC_SKIP || !__any(notconv);
+        const bool wnc = !__any(notconv);
         if (wnc && __any(b0.fl() & C_U0)) {
             unsigned m = __builtin_bit_cast(unsigned, v[0]);
 #pragma unroll
@@ -1177,13 +902,10 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         // ---- the 16 z-slots of the current brick (next brick's first value
         // in sweep order from this lane's XN row)
         float znext = S.xr[XROW16(1, RZ ? 3 : 0, lane) + (RZ ? 3 : 0)];
-        unsigned fmk = 0;
-        if (HOLD) {
-            // the position's last brick: its z-downwind node is the next brick's first (XN row) only
-            // when the run continues, else the node loaded from HBM
-            fmk = S.fmask[b0.ri()];
-            if ((b0.w1 & W1_ZD) && !(fmk & HOLD_CONT)) znext = zc;
-        }
+        // the position's last brick: its z-downwind node is the next brick's first (XN row) only
+        // when the run continues, else the node loaded from HBM
+        const unsigned fmk = S.fmask[b0.ri()];
+        if ((b0.w1 & W1_ZD) && !(fmk & HOLD_CONT)) znext = zc;
         const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
         bool changed = false, nc = false, c0 = false, c15 = false;
         if (__any(b0.fl() & F_SLOW))
@@ -1192,22 +914,6 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             brick16<RZ, false, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
         else
             brick16<RZ, false, LEAN, false>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
-#ifdef MCEIK_EXP_VALU
-        {   // sensitivity experiment: N extra dependent VALU per step (results unchanged)
-            unsigned x = (unsigned)B;
-#pragma unroll
-            for (int k = 0; k < MCEIK_EXP_VALU; k++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x));
-            asm volatile("" ::"v"(x));
-        }
-#endif
-#ifdef MCEIK_EXP_LOAD
-        if ((B & (MCEIK_EXP_LOAD - 1)) == 0) {   // sensitivity experiment: extra 64 B/lane from the u0 scratch
-            float t[4], w[4];
-            bload4(u0r, b0.seg, t);
-            bload4(u0r, b0.seg == OOB ? OOB : b0.seg + 32u, w);
-            asm volatile("" ::"v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
-        }
-#endif
         const bool val = (b0.fl() & F_VALID) != 0;
         changed = changed && val;
         notconv |= nc && val;
@@ -1220,11 +926,9 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         if (FL) {
 #pragma unroll
             for (int i = 0; i < 8; i++) asm volatile("" : "+v"(lq.a[i]), "+v"(hpnew[i]));
-        } else if (MCEIK16_PAIR) {
+        } else {
 #pragma unroll
             for (int i = 0; i < 16; i++) nn[i] = qa[i];     // raw quarters (raw_write below)
-        } else {
-            seg_finish(qa, nn);
         }
         if (HFL) {
             // the first brick loaded last step -> the other column (this
@@ -1259,16 +963,12 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         store_row16(S.xr, 0, lane, v);
         zprev = v[RZ ? 0 : 15];
         if (__any(changed)) {
-            if (MCEIK16_PAIR) {
-                float t[16];
-                raw_read(S.xr, pbr, t);
-                raw_store(ur, b0.seg, changed, t);
-            } else {
-                seg_store(ur, b0.seg, changed, v);
-            }
+            float t[16];
+            raw_read(S.xr, pbr, t);
+            raw_store(ur, b0.seg, changed, t);
         }
         TRAF(S, 3, changed, 64);
-        if (HOLD) {
+        {
             // what this lane changed: the block, its x / y faces (edge columns), its z faces (the
             // block's lowest / highest node of the column)
             const int zr = LEAN ? (b0.zb() ^ (RZ ? 1 : 0)) : b0.zb() % kb;   // brick index in the block
@@ -1279,16 +979,12 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
                 bstore1(zfr, zlo ? zf_off<float>(b0.bid(), 0, lx, ly) : OOB, v[0]);
                 bstore1(zfr, zhi ? zf_off<float>(b0.bid(), 1, lx, ly) : OOB, v[15]);
             }
-        } else if (changed) {
-            S.lastchg[b0.bid()] = (unsigned short)(clock0 + b0.clk());
         }
         load_row16(S.xr, 1, lane, v);
         if (FL) {
             line_write(S.xr, lq, hpcur);
-        } else if (MCEIK16_PAIR) {
-            raw_write(S.xr, pbn, nn);
         } else {
-            store_row16(S.xr, 1, lane, nn);
+            raw_write(S.xr, pbn, nn);
         }
         asm volatile("" ::: "memory");
         b0 = b1;
@@ -1310,13 +1006,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         }
     }
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
-    if (HOLD) {
-        // the last visits' changes (every lane is past them)
-        for (int q = max(0, nstream - g.infl + 1); q < nstream; q++) hold_settle(L, H, q % nr, clock0 + q);
-    }
-#if defined(MCEIK_ADMIT_STATS) && !MCEIK16_HOLD
-    admit_flush16(S, nr);
-#endif
+    // the last visits' changes (every lane is past them)
+    for (int q = max(0, nstream - g.infl + 1); q < nstream; q++) hold_settle(L, H, q % nr, clock0 + q);
     return nstream;
 }
 
@@ -1329,8 +1020,7 @@ __device__ __forceinline__ void verify16(const FsmLaunch &L, Rsrc ur, Rsrc u0r, 
     const float T = (float)L.conv_thresh, tolr = (float)L.tol;
     for (int base = 0; base < L.nblocks; base += 64) {
         const int k = base + lane;
-        const bool flag = k < L.nblocks && (MCEIK16_HOLD ? ((S.cbits[k >> 5] >> (k & 31)) & 1u) != 0
-                                                         : S.lastchg[k] >= 64);
+        const bool flag = k < L.nblocks && ((S.cbits[k >> 5] >> (k & 31)) & 1u) != 0;
         unsigned long long m = __ballot(flag);
         while (m) {
             const int bid = base + __builtin_ctzll(m);
@@ -1391,12 +1081,9 @@ __device__ __forceinline__ unsigned mc_group_tickets(const FsmLaunch &L, int g, 
 // (sc1: the agent-scope acquire's invalidate, which is what reaches the CU's
 // L1 -- workgroup scope (sc0) leaves a non-split workgroup's L1 alone; local
 // memory's L2 lines are not dropped by it)
-#ifndef MCEIK_MC_INV
-#define MCEIK_MC_INV "buffer_inv sc1"
-#endif
 __device__ __forceinline__ void mc_l1_invalidate()
 {
-    asm volatile(MCEIK_MC_INV "\n\ts_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
 }
 // every store issued so far has completed (reached L2) before what follows
 // is issued (the asm is also a compiler barrier: no store sinks past it)
@@ -1562,52 +1249,28 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
         const void *slow_model = reinterpret_cast<const float *>(L.slow) + sentry * ncell;
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes),
                    sr = make_rsrc(slow_model, (uint32_t)(ncell * 4));
-        const size_t zfb = MCEIK16_HOLD ? zf_bytes(L, 4) : 0;
+        const size_t zfb = zf_bytes(L, 4);
         const Rsrc zfr = make_rsrc(reinterpret_cast<char *>(L.zf) + (size_t)blockIdx.x * zfb, (uint32_t)zfb);
-        // Before the first sweep every block counts as visited and unchanged
-        // (lastproc 2 > lastchg 1) except the blocks holding boundary-condition
-        // nodes (lastchg 3): a block whose nodes and neighbours are all u_nan
-        // updates to u_nan, so it needs no visit until a neighbour changes.
-        if (!MCEIK16_HOLD) {
-            for (int t = lane; t < L.nblocks; t += 64) {
-                S.lastproc[t] = 2; S.lastchg[t] = 1;
-            }
-        }
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
 #ifdef MCEIK_TRAFFIC
         if (lane == 0)
             for (int k = 0; k < MCEIK_TRAFFIC_N; k++) S.scratch[8 + k] = 0;
 #endif
-#ifdef MCEIK_ADMIT_STATS
-        if (lane < 16) S.scratch[16 + lane] = 0;
-#endif
         unsigned nchg = 0, nsteps = 0;
         BcBoxes bc;
         bc.box = S.box;
         const bool ok = init_field<float, 1>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
-        if (MCEIK16_HOLD) {
-            hold_solve_start(L, hold_lds16(S), bc, g.nr);
-            zf_init<float>(L, zfr, u, bc);
-        } else if (lane == 0) {
-            for (int k = 0; k < bc.n; k++) {
-                const int *q = bc.box + 6 * k;
-                for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
-                    for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
-                        for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
-                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = 3;
-            }
-        }
+        // (before the first sweep only the blocks holding boundary-condition nodes are dirty: a block
+        // whose nodes and neighbours are all u_nan updates to u_nan; hold_solve_start)
+        hold_solve_start(L, hold_lds16(S), bc, g.nr);
+        zf_init<float>(L, zfr, u, bc);
         asm volatile("" ::: "memory");
         int iters = 0, ierr_last = 0;
         if (ok) {
             int sweeps_left = L.max_sweeps < 0 ? 0x7fffffff : L.max_sweeps;
             for (int it = 0; it < L.maxit && sweeps_left > 0; it++) {
                 bool notconv = false;
-                if (MCEIK16_HOLD) {
-                    hold_iter_start(L, hold_lds16(S));     // (the held stream rebases its clocks every sweep)
-                } else {
-                    iter_norm(L, S);
-                }
+                hold_iter_start(L, hold_lds16(S));     // (the held stream rebases its clocks every sweep)
                 int clock = 64;
                 for (int sw = 0; sw < 8 && sweeps_left > 0; sw++, sweeps_left--) {
                     const int rx = sw & 1, ry = (sw >> 1) & 1;
@@ -1663,10 +1326,7 @@ __device__ __forceinline__ void fsm16_body(const FsmLaunch &L)
 }
 
 // register budget: two waves per SIMD (<= 256 VGPRs)
-#ifndef MCEIK_WPE16
-#define MCEIK_WPE16 2
-#endif
-#define FSM16_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE16, MCEIK_WPE16)))
+#define FSM16_WPE __attribute__((amdgpu_waves_per_eu(2, 2)))
 template <int KB16, int CCR, bool MC>
 __global__ __launch_bounds__(64) FSM16_WPE void fsm16_solve_kernel(FsmLaunch L)
 {

@@ -9,13 +9,9 @@
 #define MCEIK_TILE 8             // 8x8 column tile = one 64-lane wave
 #define MCEIK_BRICK 512          // 8x8 columns x 8 z = one brick
 #define MCEIK_KB 4               // bricks per z-block (stream position) when the block tables fit in LDS
-#ifndef MCEIK_MAX_BLOCKS
 #define MCEIK_MAX_BLOCKS 1024    // per-block clocks in LDS: at most this many z-blocks per field
-#endif
-#ifndef MCEIK_AHEAD
-#define MCEIK_AHEAD 2            // own segments are loaded this many macro steps ahead (2 or 3;
-                                 // 3 measured 2.8% slower at C3: more visits from the longer in-flight window)
-#endif
+#define MCEIK_AHEAD 2            // own segments are loaded this many macro steps ahead (3 measured slower:
+                                 // DESIGN.md s.7, rejected variants)
 
 // One batched launch: nsolve = nmodel * nstat solves; solve id = model*nstat + station.
 struct FsmLaunch {
@@ -97,9 +93,7 @@ static inline __host__ __device__ size_t zf_bytes(const FsmLaunch &L, size_t es)
 // Debug / accounting counters in LDS: [0..3] visit statistics; MCEIK_TRAFFIC
 // builds add [8..15], the requested global-memory bytes of the wave's current
 // sweep by category (flushed to FsmLaunch.traffic after every sweep).
-#if defined(MCEIK_ADMIT_STATS)
-#define MCEIK_SCRATCH_BYTES 128  // + [16..31]: admission reason of each ring slot's position
-#elif defined(MCEIK_TRAFFIC)
+#if defined(MCEIK_TRAFFIC)
 #define MCEIK_SCRATCH_BYTES 64
 #else
 #define MCEIK_SCRATCH_BYTES 32
@@ -115,19 +109,10 @@ static inline __host__ __device__ size_t zf_bytes(const FsmLaunch &L, size_t es)
 //  9 neighbour rows XR, 10 neighbour rows XN: [2 halves][80 rows][4] R each -- row l < 64 holds lane l's
 //    8 z values (XR: its results of the last step, XN: its next brick), rows 64..79 the tile's halo columns |
 //  11 column info [nr][64] uint2 {own column offset, flags | tz | cell-cache base}
-//    (fp64 with MCEIK_F64_FL: XN is followed by HOLD [2][64] x 16 B, the held later halves of
-//    the whole-line own loads, fsm_kernel.hip line_issue64)
+//    (fp64: XN is followed by HOLD [2][64] x 16 B, the held later halves of the whole-line own
+//    loads of the compile-time-kb instances, fsm_kernel.hip line_issue64)
 #define MCEIK_CC_MAX 256         // cell-cache floats per position, upper bound
-#ifndef MCEIK_F64_FL
-#define MCEIK_F64_FL 1           // fp64 compile-time-kb instances: whole-line own loads
-#endif
 #define MCEIK_F64_HOLD (2 * 64 * 16)
-#ifndef MCEIK_BIGSTEP
-#define MCEIK_BIGSTEP 1            // fp64 early non-convergence from single big updates, u0 copies skipped after (v34; 0: A/B)
-#endif
-#ifndef MCEIK_VERIFY_EARLY_EXIT
-#define MCEIK_VERIFY_EARLY_EXIT 1  // convergence verify stops at the first failing node (0: full scan, A/B)
-#endif
 #define MCEIK_SMEM_ARRAYS 14      // (+ 12 tile frontier u8 [ntiles], 13 two block bitmaps: the held stream of
                                   //  the compact layout, fsm_hold.h)
 #define MCEIK_XROWS 80           // neighbour-row array: 64 lanes + 8 x-halo + 8 y-halo rows
@@ -188,7 +173,7 @@ static inline __host__ __device__ size_t fsm_smem_layout(const FsmLaunch &L, siz
     off[7] = o; o += MCEIK_SCRATCH_BYTES;
     off[8] = o; o += cached ? 0 : 512 * es;
     off[9] = o; o += 2 * MCEIK_XROWS * 4 * es;
-    off[10] = o; o += 2 * MCEIK_XROWS * 4 * es + (es == 8 && MCEIK_F64_FL ? MCEIK_F64_HOLD : 0);
+    off[10] = o; o += 2 * MCEIK_XROWS * 4 * es + (es == 8 ? MCEIK_F64_HOLD : 0);
     off[11] = o; o += nr * 64 * (cmp ? 4 : 8);
     return o;
 }
@@ -228,7 +213,7 @@ static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t
 }
 // LDS of one fsm16 solve wave: 0 BC boxes | 1 cell cache [nr][ccb] float | 2 tile order int [ntiles] |
 // 2 is u16 (txs | tys << 8) | 3 lastproc u16 [nblocks] | 4 lastchg u16 [nblocks] (clocks relative to the
-// iteration; with the held stream, MCEIK16_HOLD: relative to the sweep, and lastchg holds
+// iteration; with the held stream (fsm_hold.h): relative to the sweep, and lastchg holds
 // "need", the clock of the last settled change of the block or of a neighbour's face it shares) |
 // 5 ring: entry int [nr], block id int [nr], tile base u32 [nr], change mask u32 [nr] | 6 scratch |
 // 7 neighbour rows XR then XN, each [4 quarters][80 rows][4] float | 8 column meta u32 [nr][64] |
@@ -238,9 +223,7 @@ static inline __host__ __device__ bool fsm16_eligible(const FsmLaunch &L, size_t
 // floats per quarter array of the neighbour rows: 80 rows of 4 plus a 16-B pad,
 // so that the x-pair exchange (even lane: quarter 0, odd lane: quarter 1 of the
 // same row) falls in different LDS banks (unpadded, 320 floats = 5 x 64 banks)
-#ifndef MCEIK_X16PAD
 #define MCEIK_X16PAD 4
-#endif
 #define MCEIK_X16Q (MCEIK_XROWS * 4 + MCEIK_X16PAD)
 #define F16_NR (1 + (15 + MCEIK_AHEAD16 + 1) / 2)      // nr at kb16 = 2
 #define F16_CINFO 0

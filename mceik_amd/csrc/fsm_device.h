@@ -39,15 +39,11 @@ __device__ __forceinline__ void bload8(Rsrc r, uint32_t off, float (&v)[8])
     f4v b = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
-// cache policy of field stores (experiments: 2 = nt, streaming)
-#ifndef MCEIK_ST_AUX
-#define MCEIK_ST_AUX 0
-#endif
 __device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, const float (&v)[8])
 {
     f4v a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, MCEIK_ST_AUX);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), r, off + 16, 0, MCEIK_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, b), r, off + 16, 0, 0);
 }
 __device__ __forceinline__ void bload8(Rsrc r, uint32_t off, double (&v)[8])
 {
@@ -62,13 +58,13 @@ __device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, const double (&v)[
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         d2v a = {v[2 * k], v[2 * k + 1]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off + 16 * k, 0, MCEIK_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off + 16 * k, 0, 0);
     }
 }
 __device__ __forceinline__ void bstore4(Rsrc r, uint32_t off, float a0, float a1, float a2, float a3)
 {
     f4v a = {a0, a1, a2, a3};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, MCEIK_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, a), r, off, 0, 0);
 }
 __device__ __forceinline__ float bload1f(Rsrc r, uint32_t off)
 {
@@ -184,13 +180,7 @@ struct BcBoxes {
 
 // Traffic accounting (MCEIK_TRAFFIC builds): lane 0 adds bytes x (lanes where
 // pred holds) to the wave's LDS counter of category k.
-#if defined(MCEIK_TRAFFIC) && defined(MCEIK_ADMIT_STATS)
-// (the counters hold admission statistics, fsm16_kernel.hip admit_account16)
-#define TRAF(S, k, pred, bytes) do { (void)(pred); } while (0)
-#define TRAFU(S, k, bytes) do { } while (0)
-#define MCEIK_TRAF_FLUSH_ONLY
-#endif
-#if defined(MCEIK_TRAFFIC) && !defined(MCEIK_TRAF_FLUSH_ONLY)
+#ifdef MCEIK_TRAFFIC
 #define TRAF(S, k, pred, bytes)                                                                         \
     do {                                                                                                \
         const unsigned n_ = (unsigned)__builtin_popcountll(__ballot(pred));                             \
@@ -234,12 +224,9 @@ __device__ __forceinline__ void block_zcells(const FsmLaunch &L, int kb, int tz,
     ncz = (int)(((unsigned)b * L.magic_rz) >> 20) - cz0 + 1;
 }
 
-#ifndef MCEIK_LD_AUX
-#define MCEIK_LD_AUX 0
-#endif
 __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, float (&v)[4])
 {
-    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MCEIK_LD_AUX));
+    f4v a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 __device__ __forceinline__ void bload4(Rsrc r, uint32_t off, double (&v)[4])
@@ -288,10 +275,6 @@ __device__ __forceinline__ int wave_max(int v)
 // godunov_bl (a1 == UN or an overflowing / NaN candidate gives UN either way).
 // ff = f*f, ff2 = ff + ff and ff3 = 3*ff come from the caller (once per
 // slowness cell).
-#ifndef MCEIK_Y_BFI
-#define MCEIK_Y_BFI 0        // 1: godunov_v's 1D/2D-3D choice by an integer mask (A/B: no gain over
-                             // compare + select: 412.2 vs 414.1 proposals/s beside sqrt_normal's integer choice)
-#endif
 template <bool FAST>
 __device__ __forceinline__ float godunov_v(float a, float b, float c, float f, float ff, float ff2, float ff3)
 {
@@ -318,20 +301,9 @@ __device__ __forceinline__ float godunov_v(float a, float b, float c, float f, f
     const float s = FAST ? sqrt_normal(rad) : __builtin_sqrtf(rad);
     // two: 0.5 * (d2 + s); else (sm + s) * (1/3)  (same products, one multiply)
     const float y23 = ((two ? d2 : sm) + s) * (two ? 0.5f : (1.0f / 3.0f));
-    // y = (f > d2) ? y23 : f without a compare -> lane mask -> select (two
-    // hazard wait states on gfx950): d2 and f are non-negative finite floats,
-    // so bits(d2) - bits(f) < 0 exactly when f > d2; its sign smeared over
-    // the word selects y23 (v_bfi_b32: (m & y23) | (~m & f))
-#if MCEIK_Y_BFI
-    unsigned m, yb;
-    asm("v_sub_u32 %0, %1, %2" : "=v"(m) : "v"(__builtin_bit_cast(unsigned, d2)), "v"(__builtin_bit_cast(unsigned, f)));
-    asm("v_ashrrev_i32 %0, 31, %1" : "=v"(m) : "v"(m));
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(yb) : "v"(m), "v"(__builtin_bit_cast(unsigned, y23)),
-        "v"(__builtin_bit_cast(unsigned, f)));
-    const float y = __builtin_bit_cast(float, yb);
-#else
+    // (an integer-mask choice, v_bfi_b32 on the sign of bits(d2) - bits(f),
+    // measured no faster: DESIGN.md s.7, rejected variants)
     const float y = !(f > d2) ? f : y23;
-#endif
     // x >= UN, +inf or NaN -> UN: unsigned min with the bits of FLT_MAX (x >= +0)
     const unsigned ix = __builtin_bit_cast(unsigned, a1 + y);
     return __builtin_bit_cast(float, __builtin_elementwise_min(ix, 0x7f7fffffu));

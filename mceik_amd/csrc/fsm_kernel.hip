@@ -26,19 +26,10 @@
 #include "fsm_hold.h"
 #include "fsm_update.h"
 
-// the held z-block stream (fsm_hold.h) for the compact-layout fp64 instances
-#ifndef MCEIK8_HOLD
-#define MCEIK8_HOLD 1
-#endif
-// ... with its z-boundary nodes from the z-face copies (FsmLaunch.zf) instead of the field: off, measured
-// 2.4% slower in fp64 (the copies' stores and their buffer descriptor spill registers; profiles/r05_zf)
-// the step's unconverged test only until the iteration is known unconverged (brick_update NC)
-#ifndef MCEIK8_NC_SKIP
-#define MCEIK8_NC_SKIP 1
-#endif
-#ifndef MCEIK8_ZF
-#define MCEIK8_ZF 0
-#endif
+// The compact-layout fp64 instances run the held z-block stream (fsm_hold.h),
+// their z-boundary nodes read from the field (the z-face copies of the fp32
+// kernel measured 2.4% slower here: their stores and buffer descriptor spill
+// registers; profiles/r05_zf).
 
 namespace {
 
@@ -59,8 +50,8 @@ namespace {
 // neighbour's visit >= vis positions back (halo visibility).  Per-block
 // clocks live in LDS.
 // CMP (the compact layout, fsm_compact_layout(): the fp64 compile-time-kb
-// instances): 16-bit block clocks rebased at every iteration (iter_norm, as
-// fsm16_kernel.hip), and per position one meta word per lane plus the tile
+// instances): 16-bit block clocks relative to the sweep (the held stream,
+// fsm_hold.h, as fsm16_kernel.hip), and per position one meta word per lane plus the tile
 // base (ring) instead of {own column, meta} -- 25.4 -> 19.9 KB of LDS at C3,
 // 6 -> 8 resident waves per CU.
 template <typename R, bool CMP = false>
@@ -169,13 +160,9 @@ __device__ __forceinline__ BInfo brick_info(const FsmLaunch &L, int kb, const Sm
     if (zb == (RZ ? L.nzb - 1 : 0)) fl |= F_FIRST;
     if (zb == (RZ ? 0 : L.nzb - 1)) fl |= F_LAST;
     if ((meta & C_ZH) && p.zbs == 0) fl |= F_ZH;
-    // held stream: the z-boundary nodes come from the z-face copies (zf), the run end's z-downwind
-    // node of the position's last brick below the column end included
-    b.zd = CMP && MCEIK8_HOLD && valid && p.zbs == kb - 1 && !(fl & F_LAST);
-    if (CMP && MCEIK8_HOLD && MCEIK8_ZF) {
-        if (b.zh != OOB) b.zh = zf_boundary<R, RZ>(L, b.bid, false, lx, ly);
-        if (b.zd) b.zh = zf_boundary<R, RZ>(L, b.bid, true, lx, ly);
-    } else if (b.zd) {
+    // held stream: the run end's z-downwind node of the position's last brick below the column end
+    b.zd = CMP && valid && p.zbs == kb - 1 && !(fl & F_LAST);
+    if (b.zd) {
         const int zn = RZ ? zb * 8 - 1 : zb * 8 + 8;          // z-downwind node of the brick's last slot
         b.zh = ci.x + zoff_bytes<R>(zn >> 3) + (uint32_t)(zn & 7) * (uint32_t)sizeof(R);
     }
@@ -253,17 +240,11 @@ __device__ __forceinline__ void load_row(const R *x, int off0, R (&v)[8])   // o
 // Loads / stores that most lanes skip (z-upwind nodes of run starts, u0
 // copies, unchanged segments) are issued only when some lane needs them:
 // every wave-instruction costs address-unit time for all 64 lanes.
-#ifndef MCEIK_SKIP_IDLE_VMEM
-#define MCEIK_SKIP_IDLE_VMEM 1
-#endif
-// Pair-coalesced segment loads (fp32; MCEIK_PAIR_LOAD): lanes 2i and 2i+1
+// Pair-coalesced segment loads (fp32): lanes 2i and 2i+1
 // read the two 16-B halves of lane 2i's segment with one instruction and of
 // lane 2i+1's with the other, so each wave-instruction touches 32 lines
 // instead of 64; pair_finish() swaps the halves into place (DPP quad_perm
 // [1,0,3,2]) once the data has arrived.
-#ifndef MCEIK_PAIR_LOAD
-#define MCEIK_PAIR_LOAD 1
-#endif
 __device__ __forceinline__ void pair_issue(Rsrc r, uint32_t seg, float (&a)[4], float (&b)[4])
 {
     const bool odd = threadIdx.x & 1;
@@ -301,8 +282,8 @@ __device__ __forceinline__ void pair_store(Rsrc r, uint32_t seg, bool chg, const
     bstore4(r, odd ? own + 16u : oth, odd ? v[4] : x[0], odd ? v[5] : x[1], odd ? v[6] : x[2], odd ? v[7] : x[3]);
 }
 
-// ---- FL64: whole-line own loads of the fp64 compile-time-kb instances
-// (MCEIK_F64_FL).  A 128-B column line holds two 8-z fp64 bricks, which a
+// ---- FL64: whole-line own loads of the fp64 compile-time-kb instances.
+// A 128-B column line holds two 8-z fp64 bricks, which a
 // lane visits in two consecutive steps (kb even: a position's bricks pair up
 // as zbs 0/1, 2/3 in either z direction).  x-adjacent lanes (a pair) run one
 // step apart, so at every step exactly one lane of a pair -- the loader,
@@ -315,9 +296,6 @@ __device__ __forceinline__ void pair_store(Rsrc r, uint32_t seg, bool chg, const
 // As fsm16's FL, with the held half in LDS instead of registers (this
 // instance runs at its VGPR limit).  Without it a line was read as two 64-B
 // halves a step apart and the L2 re-fetched part of them in between.
-#ifndef MCEIK_ROTATE
-#define MCEIK_ROTATE 0
-#endif
 #define XHOLD(k) (XROW(2, 0, 0) + (k) * 128)         // HOLD quarter k of lane l: 2 values at + 2 l
 __device__ __forceinline__ void line_issue64(Rsrc r, uint32_t lseg, bool isl, double (&a)[4], double (&h)[4],
                                              int &rowl, int &rowo)
@@ -448,9 +426,6 @@ __device__ __forceinline__ int decide(const FsmLaunch &L, const Smem<R, CMP> &S,
     }
     if (st.wait > 0) {
         st.wait--;
-#ifdef MCEIK_BUBBLESTATS
-        if (threadIdx.x == 0) S.scratch[3]++;          // experiment: bubble positions
-#endif
         return -1;
     }
     const int kz = st.k;
@@ -498,7 +473,7 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R, 
         nbv = min(kb, L.nzb - tz * kb);
         // first visit of the block in this iteration: no visit since the iteration's first clock
         // (held stream: its clocks restart every sweep, the iteration's visits are a bitmap)
-        const int u0flag = (CMP && MCEIK8_HOLD) ? !((S.vbits[bid >> 5] >> (bid & 31)) & 1u)
+        const int u0flag = CMP ? !((S.vbits[bid >> 5] >> (bid & 31)) & 1u)
                                                 : (int)S.lastproc[bid] < clock_it;
         if ((entry & 0xffffff) != ct.tile) column_tile<R>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         ci.x = ct.col;
@@ -516,7 +491,7 @@ __device__ __forceinline__ void admit(const FsmLaunch &L, int kb, const Smem<R, 
         if (CMP) S.ring[2 * L.nr + ri] = (int)tbase;
         if (entry >= 0) {
             S.lastproc[bid] = (typename Smem<R, CMP>::clk_t)clock;
-            if (CMP && MCEIK8_HOLD) S.vbits[bid >> 5] |= 1u << (bid & 31);
+            if (CMP) S.vbits[bid >> 5] |= 1u << (bid & 31);
             if (L.visit_stats) {
                 S.scratch[0] += nbv;
                 S.scratch[1] += nbv * nact;
@@ -565,8 +540,8 @@ __device__ __forceinline__ void gather_xy(const FsmLaunch &L, const Smem<R, CMP>
 // sweep-order first/last brick, no lane holds a BC node, and every lane's
 // missing x/y neighbours are already its own old values (column_info).
 // NC: evaluate the unconverged test (nc); the sweep drops it once a lane of
-// the wave has found the iteration unconverged (MCEIK8_NC_SKIP: the outcome
-// cannot change, as for the u0 copies under MCEIK_BIGSTEP)
+// the wave has found the iteration unconverged (the outcome cannot change, as
+// for the fp64 u0 copies skipped after a big step)
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, bool GENERIC, bool CMP, bool NC = true>
 __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, CMP> &S, const BInfo &b0, R (&c)[8],
                                              R (&n)[8], R (&r)[8], R zc, int lx, int ly, int rx, int ry,
@@ -575,7 +550,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
 {
     const int lane = threadIdx.x;
     const R T = (R)L.conv_thresh;
-    // MCEIK_BIGSTEP (fp64): a node that drops by >= tol (1 + 2^-50) in one
+    // fp64 (v34, "big step"): a node that drops by >= tol (1 + 2^-50) in one
     // update moved by >= tol over the iteration (values only fall), so the
     // reference's |u0 - u| < tol fails: not converged, as the >= T rule says
     // in fp32 (where T = 2^26 s makes that rule empty in fp64)
@@ -663,7 +638,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
             nv = fmin_(self, godunov_v<FAST>(ux, uy, uz, fv, ffv, CELLF ? ff2c : ffv + ffv, CELLF ? ff3c : (R)3 * ffv));
         }
         const bool dec = nv < self;
-        if (NC) nc |= dec && (self >= T || (MCEIK_BIGSTEP && sizeof(R) == 8 && self - nv >= TB));
+        if (NC) nc |= dec && (self >= T || (sizeof(R) == 8 && self - nv >= TB));
         changed |= dec;
         if (pj == 0) c0 = dec;               // the brick's lowest / highest node changed (z faces of
         if (pj == 7) c7 = dec;               //   its block, held stream)
@@ -678,11 +653,10 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
 // (the ring then has nr = 2 + 16 / KB slots); 0: runtime L.kb / L.nr.
 // nchg: per-lane count of changed column segments (visit statistics).
 template <typename R, int SLOWMODE, bool FAST, bool RZ, int ZSH, int CCR, int KB, bool CMP>
-__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, Rsrc zfr, const BcBoxes &bc,
+__device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc sr, const BcBoxes &bc,
                                      const Smem<R, CMP> &S, int rx, int ry, int clock_it, int clock0,
                                      bool &notconv, int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
-    const Rsrc zr_ = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? zfr : ur;   // where the z-boundary nodes are read
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const R UN = Num<R>::unan();
@@ -703,7 +677,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     Stream st;
     st.cursor = 0; st.tile = -1; st.k = 0; st.k0 = 0; st.wait = 0;
     // the held stream (compact layout; fsm_hold.h): clocks restart at 64 every sweep
-    constexpr bool HOLD = CMP && MCEIK8_HOLD;
+    constexpr bool HOLD = CMP;
     // (its scan state -- first incomplete tile, previous position's tile -- lives in LDS scratch
     // [4], [5]: fewer scalar registers live across the step loop)
     // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
@@ -728,25 +702,24 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             return decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
         }
     };
-    R c[8], n[8], q[8], p[8], r[8], fq[8], hq[4], hn[4];
-    constexpr bool PAIR = MCEIK_PAIR_LOAD && sizeof(R) == 4 && MCEIK_AHEAD == 2;
+    R c[8], n[8], q[8], r[8], fq[8], hq[4], hn[4];
+    constexpr bool PAIR = sizeof(R) == 4;
     // FL64: whole-line own loads (line_issue64): la / lh this step's quarters
     // of the loader's now / later half, rowl / rowo the XN rows they go to
-    constexpr bool FL64 = MCEIK_F64_FL && sizeof(R) == 8 && KB > 0 && (KB & 1) == 0 && MCEIK_AHEAD == 2 &&
-                          !MCEIK_ROTATE;
+    constexpr bool FL64 = sizeof(R) == 8 && KB > 0 && (KB & 1) == 0;
     double la[4], lh[4];
     int rowl = 0, rowo = 0;
     float qa[4], qb[4];                  // PAIR: raw halves of q
-    R zc, zn, zq, zp;                // z-upwind values of run starts (vb .. vb+3)
+    R zc, zn, zq;                    // z-upwind values of run starts (vb .. vb+2)
     float ccv[CCR];
     int ccsize = 0;
     ColTile ct;
     ct.tile = -1;
     // prologue decisions: the positions of lane (0,0)'s bricks 0..AH-1; the
-    // loop then decides position (B+AH)/kb (own segments are loaded AH steps
-    // ahead, MCEIK_AHEAD = 2)
+    // loop then decides position (B+AH)/kb (own segments are loaded AH = 2
+    // steps ahead)
     int ndecided = 0, nstream = 0x7fffffff, dri = 0;
-    constexpr int AH = MCEIK_AHEAD;      // own segments loaded AH steps ahead (2 or 3)
+    constexpr int AH = MCEIK_AHEAD;      // own segments loaded AH = 2 steps ahead
     for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
         int zh;
         const int e = decide_any(pos, dri, zh);
@@ -765,8 +738,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (++dri == nr) dri = 0;
     }
     asm volatile("" ::: "memory");
-    // Brick info of vb (b0), vb+1 (b1) [and vb+2 (b2) when AH = 3]; the loop
-    // computes vb+AH's (b3) once, uses its offsets for the own-segment
+    // Brick info of vb (b0), vb+1 (b1); the loop computes vb+AH's (b3) once, uses its offsets for the own-segment
     // prefetch and carries it (one column-info read and decode per brick).
     Pos p3;
     pos_init(p3, -d, kb, nr);
@@ -781,7 +753,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         bload4(ur, ho, hq);
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
-    zc = bload1(zr_, b0.zh, R());
+    zc = bload1(ur, b0.zh, R());
     TRAF(S, 0, b0.seg != OOB, 8 * sizeof(R));
     TRAF(S, 2, b0.zh != OOB, sizeof(R));
     pos_adv(p3, kb, nr);
@@ -793,16 +765,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         bload4(ur, ho, hn);   // halos of vb+1
         TRAF(S, 1, ho != OOB, 4 * sizeof(R));
     }
-    zn = bload1(zr_, b1.zh, R());
+    zn = bload1(ur, b1.zh, R());
     TRAF(S, 0, b1.seg != OOB, 8 * sizeof(R));
     TRAF(S, 2, b1.zh != OOB, sizeof(R));
-    BInfo b2;
-    if (AH == 3) {
-        pos_adv(p3, kb, nr);
-        b2 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, cinfo_at(L, S, p3.ri, lane, lanecol));
-        bload8(ur, b2.seg, q);
-        zq = bload1(zr_, b2.zh, R());
-    }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         r[i] = UN;
@@ -840,34 +805,15 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #pragma unroll
     for (int i = 0; i < 4; i++) asm volatile("" : "+v"(hq[i]));
     asm volatile("" : "+v"(zc), "+v"(zn));
-    if (AH == 3) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) asm volatile("" : "+v"(q[i]));
-        asm volatile("" : "+v"(zq));
-    }
     asm volatile("" ::: "memory");
 
     int ph = AH % kb;                // (B + AH) mod kb: 0 when lane (0,0)'s vb+AH starts a new position
-    // MCEIK_ROTATE (compile-time kb only): two steps per loop iteration with
-    // the roles of the brick (c/n) and halo (hq/hn) registers swapped, so
-    // neither is copied between steps and a halo load is first waited for
-    // when it is staged, one step after it was issued
-#ifndef MCEIK_ROTATE
-#define MCEIK_ROTATE 0       // measured 1% slower at C3 (v17), kept as an option
-#endif
-    constexpr bool ROT = MCEIK_ROTATE && KB > 0;
-#ifndef MCEIK_CC_DEFER
-#define MCEIK_CC_DEFER 1
-#endif
     int cc_pend = -1;                // ring slot whose cell loads (ccv) are written next step
     int B = 0;
-    // MCEIK_BOTTOM_EXIT: the stream decision for step B is made at the end of
-    // step B-1 (after its write-back, so it reads the same block clocks) and
-    // the loop tests its exit at the bottom: one path around the loop, so the
-    // loop-carried registers need no phi copies on a second edge
-#ifndef MCEIK_BOTTOM_EXIT
-#define MCEIK_BOTTOM_EXIT 1
-#endif
+    // The stream decision for step B is made at the end of step B-1 (after
+    // its write-back, so it reads the same block clocks) and the loop tests
+    // its exit at the bottom: one path around the loop, so the loop-carried
+    // registers need no phi copies on a second edge
     bool ccfill = false;
     int ccri = 0;
     auto decide_step = [&]() __attribute__((always_inline)) {
@@ -897,10 +843,6 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         return !(nstream != 0x7fffffff && B >= nstream * kb + 14);
     };
     auto step = [&](R (&c)[8], R (&n)[8], R (&hq)[4], R (&hn)[4]) __attribute__((always_inline)) -> bool {
-        if (!MCEIK_BOTTOM_EXIT) {
-            decide_step();
-            if (!more()) return false;
-        }
         // ---- prefetch: own segment and halos of vb+AH (consumed at the end
         // of this step, before its stores; halos staged to LDS at the end of
         // the next), slowness of vb+1 (modes 0/1)
@@ -911,18 +853,13 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         const u2v ci3 = cinfo_at(L, S, p3.ri, lane, lanecol), cie = cinfo_at(L, S, pe.ri, he, hcol);
         __builtin_amdgcn_sched_barrier(0);     // keep the two reads ahead of every use
         const BInfo b3 = brick_info<R, RZ, ZSH>(L, kb, S, p3, nstream, lx, ly, bc, ci3);
-        if (AH == 3) {
-            bload8(ur, b3.seg, p);
-            zp = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(zr_, b3.zh, R()) : R(0);
-        } else {
-            if (PAIR)
-                pair_issue(ur, b3.seg, qa, qb);
-            else if (FL64)
-                line_issue64(ur, b3.lseg, p3.vb >= 0 && (p3.zbs & 1) == 0, la, lh, rowl, rowo);
-            else
-                bload8(ur, b3.seg, q);
-            zq = (!MCEIK_SKIP_IDLE_VMEM || __any(b3.zh != OOB)) ? bload1(zr_, b3.zh, R()) : R(0);
-        }
+        if (PAIR)
+            pair_issue(ur, b3.seg, qa, qb);
+        else if (FL64)
+            line_issue64(ur, b3.lseg, p3.vb >= 0 && (p3.zbs & 1) == 0, la, lh, rowl, rowo);
+        else
+            bload8(ur, b3.seg, q);
+        zq = __any(b3.zh != OOB) ? bload1(ur, b3.zh, R()) : R(0);
         {
             const uint32_t ho = halo_offset<R, RZ>(L, kb, pe, nstream, hh, cie, hbit, hdelta);
             bload4(ur, ho, hn);
@@ -939,7 +876,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         if (__any(b0.fl & F_SLOW))
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, true>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                            ierr_last, zdsel, c0, c7);
-        else if (!MCEIK8_NC_SKIP || !__any(notconv))
+        else if (!__any(notconv))
             brick_update<R, SLOWMODE, FAST, RZ, ZSH, false>(L, S, b0, c, n, r, zc, lx, ly, rx, ry, changed, nc,
                                                             ierr_last, zdsel, c0, c7);
         else
@@ -961,7 +898,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             // cells of the position admitted one step earlier: lane (0,0)
             // enters it at the next step, so a step of latency cover is free
             // (kb >= 2: the next admission, which reloads ccv, is >= 2 steps on)
-            if (MCEIK_CC_DEFER && kb >= 2) {
+            if (kb >= 2) {
                 if (cc_pend >= 0) cc_write<R, CCR>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
                 cc_pend = ccfill ? ccri : -1;
             } else if (ccfill) {
@@ -979,24 +916,23 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 if (!FL64) nn[i] = q[i];
-                if (AH == 3) q[i] = p[i];
             }
         }
         // u0: a block's first visit in the iteration (old values c)
-        // (MCEIK_BIGSTEP: once the iteration is known unconverged its
-        // verify never runs, so its remaining u0 copies are not needed)
+        // (once the iteration is known unconverged its verify never runs, so
+        // its remaining u0 copies are not needed)
         auto u0_store = [&]() __attribute__((always_inline)) {
-            if ((!MCEIK_SKIP_IDLE_VMEM || __any(b0.fl & C_U0)) && !(MCEIK_BIGSTEP && __any(notconv))) {
+            if (__any(b0.fl & C_U0) && !__any(notconv)) {
                 R m = fmin_(fmin_(fmin_(c[0], c[1]), fmin_(c[2], c[3])), fmin_(fmin_(c[4], c[5]), fmin_(c[6], c[7])));
                 const bool st0 = m < (R)L.conv_thresh && (b0.fl & C_U0);
-                if (!MCEIK_SKIP_IDLE_VMEM || __any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
+                if (__any(st0)) bstore8(u0r, st0 ? b0.seg : OOB, c);
                 TRAF(S, 4, st0, 8 * sizeof(R));
             }
         };
         // neighbour rows for the next step: this step's results, the next brick
         // (fp64: the brick of the next step is read back from the XN row first,
         // so c's u0 copy is stored before)
-        constexpr bool LAZYN = sizeof(R) == 8 && !ROT;
+        constexpr bool LAZYN = sizeof(R) == 8;
         if (LAZYN) u0_store();
         store_row(S.xr, 0, lane, r);
         if (LAZYN) load_row(S.xr, XROW(1, 0, lane), c);
@@ -1004,12 +940,9 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             line_write64(reinterpret_cast<double *>(S.xr), rowl, rowo, la, lh);
         else
             store_row(S.xr, 1, lane, nn);
-        if (!ROT) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) hq[i] = hn[i];
-        }
+        for (int i = 0; i < 4; i++) hq[i] = hn[i];
         zc = zn; zn = zq;
-        if (AH == 3) zq = zp;
         // materialise the copies here (the loads' waits land here, before the
         // stores); otherwise they become the loop's phi copies at the latch
 #pragma unroll
@@ -1020,12 +953,12 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 #pragma unroll
             for (int i = 0; i < 4; i++) asm volatile("" : "+v"(la[i]), "+v"(lh[i]));
         }
-        if (!ROT) asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]));
+        asm volatile("" : "+v"(hq[0]), "+v"(hq[1]), "+v"(hq[2]), "+v"(hq[3]));
         asm volatile("" : "+v"(zn));
         asm volatile("" ::: "memory");
 
         // ---- write-back, u0 at a block's first visit of the iteration, change stamps
-        if (!MCEIK_SKIP_IDLE_VMEM || __any(changed)) {
+        if (__any(changed)) {
             if (PAIR)
                 pair_store(ur, b0.seg, changed, reinterpret_cast<const float (&)[8]>(r));
             else
@@ -1039,61 +972,28 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             const int zr = (b0.zb8 >> 3) % kb;                     // brick index in the block
             const bool zlo = changed && zr == 0 && c0, zhi = changed && zr == kb - 1 && c7;
             if (changed) atomicOr(&S.fmask[b0.ri], xyface | (zlo ? HOLD_ZLO : 0u) | (zhi ? HOLD_ZHI : 0u));
-            // the block's lowest / highest node of this column changed: its z-face copy too
-            if (MCEIK8_ZF && __any(zlo || zhi)) {
-                bstore1(zfr, zlo ? zf_off<R>(b0.bid, 0, lx, ly) : OOB, r[0]);
-                bstore1(zfr, zhi ? zf_off<R>(b0.bid, 1, lx, ly) : OOB, r[7]);
-            }
         } else if (changed) {
             S.lastchg[b0.bid] = (typename Smem<R, CMP>::clk_t)(clock0 + b0.clk);   // lanes of one block write the same value
         }
         asm volatile("" ::: "memory");
+        if (!LAZYN) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            if (ROT) {
-                c[i] = nn[i];            // c's registers become the next step's n
-            } else if (LAZYN) {
-            } else {
+            for (int i = 0; i < 8; i++) {
                 c[i] = n[i];
                 n[i] = nn[i];
             }
         }
         b0 = b1;
-        if (AH == 3) {
-            b1 = b2;
-            b2 = b3;
-        } else {
-            b1 = b3;
-        }
+        b1 = b3;
         if (++ph == kb) ph = 0;
         B++;
-        if (MCEIK_BOTTOM_EXIT) {
-            decide_step();
-            return more();
-        }
-        return true;
-    };
-    if (MCEIK_BOTTOM_EXIT) {
         decide_step();
-        if (more()) {
-            if (ROT) {
-                for (;;) {
-                    if (!step(c, n, hq, hn)) break;
-                    if (!step(n, c, hn, hq)) break;
-                }
-            } else {
-                do {
-                } while (step(c, n, hq, hn));
-            }
-        }
-    } else if (ROT) {
-        for (;;) {
-            if (!step(c, n, hq, hn)) break;
-            if (!step(n, c, hn, hq)) break;
-        }
-    } else {
-        while (step(c, n, hq, hn)) {
-        }
+        return more();
+    };
+    decide_step();
+    if (more()) {
+        do {
+        } while (step(c, n, hq, hn));
     }
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     if constexpr (HOLD) {
@@ -1103,42 +1003,6 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     }
     return nstream;
 }
-
-// Start of an iteration (compact layout): every block's pending state (it
-// changed at its last visit, or a face neighbour changed since) becomes
-// lastchg 1 / 0 against lastproc 1 and the clock restarts at 64
-// (fsm16_kernel.hip iter_norm; nothing is in flight across an iteration
-// boundary, so the decisions are those of unbounded clocks).
-template <typename R>
-__device__ __forceinline__ void iter_norm(const FsmLaunch &L, const Smem<R, true> &S)
-{
-    const int nt = L.ntiles, nzk = L.nzk;
-    unsigned pend = 0;                       // bit i: block lane + 64 i (nblocks <= 1024)
-    for (int i = 0; i * 64 < L.nblocks; i++) {
-        const int b = threadIdx.x + 64 * i;
-        if (b >= L.nblocks) break;
-        const int tz = b / nt, id = b - tz * nt, ty = id / L.ntx, tx = id - ty * L.ntx;
-        const int lp = S.lastproc[b];
-        bool d = S.lastchg[b] >= lp;
-        if (tx > 0) d |= S.lastchg[b - 1] > lp;
-        if (tx < L.ntx - 1) d |= S.lastchg[b + 1] > lp;
-        if (ty > 0) d |= S.lastchg[b - L.ntx] > lp;
-        if (ty < L.nty - 1) d |= S.lastchg[b + L.ntx] > lp;
-        if (tz > 0) d |= S.lastchg[b - nt] > lp;
-        if (tz < nzk - 1) d |= S.lastchg[b + nt] > lp;
-        if (d) pend |= 1u << i;
-    }
-    asm volatile("" ::: "memory");
-    for (int i = 0; i * 64 < L.nblocks; i++) {
-        const int b = threadIdx.x + 64 * i;
-        if (b >= L.nblocks) break;
-        S.lastproc[b] = 1;
-        S.lastchg[b] = (unsigned short)((pend >> i) & 1u);
-    }
-    asm volatile("" ::: "memory");
-}
-template <typename R>
-__device__ __forceinline__ void iter_norm(const FsmLaunch &, const Smem<R, false> &) {}
 
 // End-of-iteration check of the nodes below T (run only when no node >= T
 // changed): the z-blocks that changed in this iteration (lastchg >= the
@@ -1150,8 +1014,8 @@ __device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u
     const R T = (R)L.conv_thresh, tolr = (R)L.tol;
     for (int base = 0; base < L.nblocks; base += 64) {
         const int k = base + lane;
-        const bool flag = k < L.nblocks && ((CMP && MCEIK8_HOLD) ? ((S.cbits[k >> 5] >> (k & 31)) & 1u) != 0
-                                                                 : S.lastchg[k] >= clock_it);
+        const bool flag = k < L.nblocks && (CMP ? ((S.cbits[k >> 5] >> (k & 31)) & 1u) != 0
+                                                 : S.lastchg[k] >= clock_it);
         unsigned long long m = __ballot(flag);
         while (m) {
             const int bid = base + __builtin_ctzll(m);
@@ -1175,19 +1039,14 @@ __device__ __forceinline__ void verify_small(const FsmLaunch &L, Rsrc ur, Rsrc u
             }
             // the iteration is not converged once any node fails: the rest of
             // the scan cannot change the answer (its only output), so stop
-            if (MCEIK_VERIFY_EARLY_EXIT && __any(notconv)) return;
+            if (__any(notconv)) return;
         }
     }
 }
 
-// MCEIK_WPE (experiments): register budget for that many waves per SIMD
-#ifdef MCEIK_WPE
-#define FSM_WPE __attribute__((amdgpu_waves_per_eu(MCEIK_WPE, MCEIK_WPE)))
-#else
 // fp64: two waves per SIMD (the register budget that allows it: 4 B of
 // spills outside the step loop, against one wave with AGPR spills)
 #define FSM_WPE __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 ? 2 : 1)))
-#endif
 template <typename R, int SLOWMODE, bool FAST, int ZSH, int CCR, int KB>
 __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
 {
@@ -1225,21 +1084,17 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
             slow_bytes = (uint32_t)(ncell * 4);
         }
         const Rsrc ur = make_rsrc(u, fbytes), u0r = make_rsrc(u0, fbytes), sr = make_rsrc(slow_model, slow_bytes);
-        const size_t zfb = (CMP && MCEIK8_HOLD && MCEIK8_ZF) ? zf_bytes(L, sizeof(R)) : 0;
-        const Rsrc zfr = make_rsrc(reinterpret_cast<char *>(L.zf) + (size_t)blockIdx.x * zfb, (uint32_t)zfb);
         // Clocks before the first sweep: every block "visited" at -2 and
         // unchanged since (-3), except the blocks holding boundary-condition
         // nodes (changed at -1).  Exact: a block whose nodes and neighbours
         // are all u_nan updates to u_nan (a1 == u_nan), so it needs no visit
         // until a neighbour changes.  The stream clock starts at 64, so no
         // initial visit counts as in flight.
-        // (compact layout: 16-bit clocks relative to the iteration, the same
-        // order -- visited 2, changed 1, BC blocks changed 3 -- rebased by
-        // iter_norm at every iteration start, where the clock restarts at 64)
-        constexpr bool HOLD = CMP && MCEIK8_HOLD;
+        // (compact layout: the held stream, hold_solve_start)
+        constexpr bool HOLD = CMP;
         if (!HOLD) {
             for (int t = lane; t < L.nblocks; t += 64) {
-                S.lastproc[t] = CMP ? 2 : -2; S.lastchg[t] = CMP ? 1 : -3;
+                S.lastproc[t] = -2; S.lastchg[t] = -3;
             }
         }
         if (lane == 0) { S.scratch[0] = 0; S.scratch[1] = 0; S.scratch[2] = 0; S.scratch[3] = 0; }
@@ -1253,14 +1108,13 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
         const bool ok = init_field<R, SLOWMODE>(L, u, ur, slow_model, L.src + (size_t)station * L.nsrc * 4, bc);
         if constexpr (HOLD) {
             hold_solve_start(L, hold_lds(S), bc, L.nr);
-            if (MCEIK8_ZF) zf_init<R>(L, zfr, u, bc);
         } else if (lane == 0) {
             for (int k = 0; k < bc.n; k++) {
                 const int *q = bc.box + 6 * k;
                 for (int tz = q[4] / (8 * L.kb); tz <= q[5] / (8 * L.kb); tz++)
                     for (int ty = q[2] >> 3; ty <= q[3] >> 3; ty++)
                         for (int tx = q[0] >> 3; tx <= q[1] >> 3; tx++)
-                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = CMP ? 3 : -1;
+                            S.lastchg[(tz * L.nty + ty) * L.ntx + tx] = -1;
             }
         }
         asm volatile("" ::: "memory");
@@ -1271,9 +1125,6 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                 bool notconv = false;
                 if constexpr (HOLD) {
                     hold_iter_start(L, hold_lds(S));      // (the held stream rebases its clocks every sweep)
-                    clock = 64;
-                } else if (CMP) {
-                    iter_norm(L, S);
                     clock = 64;
                 }
                 const int clock_it = clock;
@@ -1286,11 +1137,11 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                     // never in flight (nor within vis) for the next one
                     if (sw & 4)
                         clock += L.infl + sweep<R, SLOWMODE, FAST, true, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, zfr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
+                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
                                               nsteps);
                     else
                         clock += L.infl + sweep<R, SLOWMODE, FAST, false, ZSH, CCR, KB>(
-                                              L, ur, u0r, sr, zfr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
+                                              L, ur, u0r, sr, bc, S, rx, ry, clock_it, clock, notconv, ierr_last, nchg,
                                               nsteps);
 #ifdef MCEIK_STEPSTATS
                     {   // experiment: visited blocks of this sweep that did not change
@@ -1329,12 +1180,8 @@ __global__ __launch_bounds__(64) FSM_WPE void fsm_solve_kernel(FsmLaunch L)
                 atomicAdd(L.visit_stats + 2, (unsigned long long)(unsigned)S.scratch[3]);
 #else
                 atomicAdd(L.visit_stats + 1, (unsigned long long)(unsigned)S.scratch[1]);
-#ifdef MCEIK_BUBBLESTATS
-                atomicAdd(L.visit_stats + 2, (unsigned long long)(unsigned)S.scratch[3]);
-#else
                 atomicAdd(L.visit_stats + 2, (unsigned long long)nchg);
                 atomicAdd(L.visit_stats + 3, (unsigned long long)nsteps);
-#endif
 #endif
             }
         }

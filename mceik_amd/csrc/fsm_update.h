@@ -6,13 +6,6 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
-#ifndef MCEIK_SQRT_ADD3_ASM
-#define MCEIK_SQRT_ADD3_ASM 0     // 1: the add as an asm statement too (the compiler pads its use: +0.2% slower, tools A/B)
-#endif
-#ifndef MCEIK_SQRT_INT
-#define MCEIK_SQRT_INT 1     // sqrt_normal's rounding choice in integer arithmetic (0: compares + selects)
-#endif
-
 namespace {
 
 template <typename R> struct Num;
@@ -60,19 +53,13 @@ __device__ __forceinline__ double godunov(double a, double b, double c, double f
     return UN;
 }
 
-// The same update without branches (MCEIK_F64_SELECT): the sorted triple by
+// The same update without branches: the sorted triple by
 // min / max / median, the 1D, 2D and 3D candidates all computed, the
 // reference's choice made by selects.  Values and ierr identical to godunov()
 // (inputs are never NaN; a root of a negative radicand is NaN only in a
 // candidate that is not selected, or gives the reference's ierr 3).  A wave
 // whose lanes take different branches runs every branch anyway; this form
 // drops the exec-mask bookkeeping and branches of the divergent code.
-#ifndef MCEIK_F64_SELECT
-#define MCEIK_F64_SELECT 1
-#endif
-#ifndef MCEIK_F64_ONE_SQRT
-#define MCEIK_F64_ONE_SQRT 0     // 1: one square root per node (bitwise; measured 13% slower, profiles/r03_f64one)
-#endif
 __device__ __forceinline__ double godunov_sel(double a, double b, double c, double f, int &ierr)
 {
     const double UN = DBL_MAX;
@@ -82,40 +69,6 @@ __device__ __forceinline__ double godunov_sel(double a, double b, double c, doub
     const double x1 = a1 + f;
     const double amb = a1 - a2;
     const double arg = (2.0 * f) * f - amb * amb;
-#if MCEIK_F64_ONE_SQRT
-    // One square root per node.  The reference takes the 3D root when the 2D
-    // value x2 = 0.5*((a1 + a2) + sqrt(arg)) exceeds a3 (|a1 - a2| < f), i.e.
-    // when sqrt(arg) > T = 2*a3 - (a1 + a2).  Outside a band of half-width
-    // E = 2^-40 * (a1 + a2 + 2*a3 + 2*f) around T -- 2^11 times the rounding
-    // of every quantity involved (all of them are sums of a1..a3, f and
-    // sqrt(arg) <= sqrt(2) f) -- comparing arg with (T +- E)^2 gives the
-    // reference's decision on its rounded x2, so only the chosen radicand is
-    // square-rooted.  Inside the band (and for non-finite T or E) the lane
-    // decides on the literal x2.  Values and ierr identical to godunov().
-    const bool use2 = __builtin_fabs(amb) < f;
-    const double S = a1 + a2;
-    const double x2b = (a1 < a2 ? a1 : a2) + f;
-    const double T = 2.0 * a3 - S;
-    const double E = 0x1p-40 * ((S + 2.0 * a3) + 2.0 * f);
-    const double tp = T + E, tm = T - E;
-    const bool fin = E < 0x1p400;                           // T, E and their squares are finite
-    const bool open3 = a3 == UN;                            // x2 is finite: never above DBL_MAX
-    const bool sure3 = fin && !open3 && (tp < 0.0 || arg > tp * tp);   // sqrt(arg) > T + E: x2 > a3
-    const bool sure2 = open3 || (fin && tm > 0.0 && arg < tm * tm);    // sqrt(arg) < T - E: x2 < a3
-    const bool r1 = !(x1 > a2), nan_in = a1 == UN;
-    bool d3 = use2 ? sure3 : x2b > a3;                      // the reference's 3D case
-    if (use2 && !(sure3 || sure2)) d3 = 0.5 * (S + __builtin_sqrt(arg)) > a3;   // the band: its literal test
-    const double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
-    const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
-    const double disc = qb * qb - 4.0 * qc;
-    const double sq = __builtin_sqrt(d3 ? disc : arg);
-    const double x2 = use2 ? 0.5 * (S + sq) : x2b;
-    const double x3 = 0.5 * (-qb + sq);
-    const bool in3 = x3 < UN;
-    const int e3 = in3 ? (x3 < 0.0 ? 2 : (disc < 0.0 ? 1 : 0)) : 3;
-    ierr = (nan_in || r1 || !d3) ? 0 : e3;
-    return nan_in ? UN : r1 ? x1 : !d3 ? x2 : (in3 ? x3 : UN);
-#else
     const double x2 = __builtin_fabs(amb) < f ? 0.5 * ((a1 + a2) + __builtin_sqrt(arg)) : (a1 < a2 ? a1 : a2) + f;
     const double qb = -((2.0 / 3.0) * ((a1 + a2) + a3));
     const double qc = ((((a1 * a1) + (a2 * a2)) + (a3 * a3)) - f * f) * (1.0 / 3.0);
@@ -126,7 +79,6 @@ __device__ __forceinline__ double godunov_sel(double a, double b, double c, doub
     const int e3 = in3 ? (x3 < 0.0 ? 2 : (disc < 0.0 ? 1 : 0)) : 3;
     ierr = (nan_in || r1 || r2) ? 0 : e3;
     return nan_in ? UN : r1 ? x1 : r2 ? x2 : (in3 ? x3 : UN);
-#endif
 }
 
 // Correctly rounded sqrt for normal positive x (LLVM's expansion without the
@@ -143,54 +95,19 @@ __device__ __forceinline__ double godunov_sel(double a, double b, double c, doub
 // bits, +-0 and negatives do not).  Same values as the compare/select form
 // without its compare -> lane-mask -> select hazard wait states (gfx950 puts
 // two wait states between a VALU write of an SGPR mask and its use).
-#ifndef MCEIK_SQRT_ONESIDED
-#define MCEIK_SQRT_ONESIDED 0    // 1: only the upper test (v_sqrt_f32 never above the correctly rounded
-                                 // root), -1: only the lower test (never below); see tools/sqrt_dir_probe.hip
-#endif
 __device__ __forceinline__ float sqrt_normal(float x)
 {
     const float s = __builtin_amdgcn_sqrtf(x);
     const int sb = __builtin_bit_cast(int, s);
-#if MCEIK_SQRT_ONESIDED != 0
-    {
-        // The exhaustive probe (tools/sqrt_dir_probe.hip) shows the hardware
-        // root is off by at most one ulp and only on one side over the domain
-        // x >= 2^-104, so one Tuckerman test decides: +1 ulp when x > up*s
-        // (MCEIK_SQRT_ONESIDED 1), -1 ulp unless x > dn*s (-1).
-        const float t = __builtin_bit_cast(float, sb + MCEIK_SQRT_ONESIDED);
-        const int e = __builtin_bit_cast(int, __builtin_fmaf(-t, s, x));
-        int p;
-        asm("v_med3_i32 %0, %1, 0, 1" : "=v"(p) : "v"(e));
-        return __builtin_bit_cast(float, MCEIK_SQRT_ONESIDED > 0 ? sb + p : (sb - 1) + p);
-    }
-#endif
     const float dn = __builtin_bit_cast(float, sb - 1);
     const float up = __builtin_bit_cast(float, sb + 1);
     const int edn = __builtin_bit_cast(int, __builtin_fmaf(-dn, s, x));
     const int eup = __builtin_bit_cast(int, __builtin_fmaf(-up, s, x));
-#if MCEIK_SQRT_INT
     // (asm: the instruction selector turns the clamp back into compares + carry adds)
-    int pdn, pup, r;
-#if MCEIK_SQRT_ADD3_ASM == 2
-    // one asm statement: the compiler pads a use of an asm result by a wait
-    // state (it cannot see whether the asm wrote a transcendental result), so
-    // the three instructions are one block and only r's use can be padded
-    asm("v_med3_i32 %1, %3, 0, 1\n\tv_med3_i32 %2, %4, 0, 1\n\tv_add3_u32 %0, %5, %1, %2"
-        : "=v"(r), "=&v"(pdn), "=&v"(pup) : "v"(edn), "v"(eup), "v"(sb - 1));
-#else
+    int pdn, pup;
     asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pdn) : "v"(edn));
     asm("v_med3_i32 %0, %1, 0, 1" : "=v"(pup) : "v"(eup));
-#if MCEIK_SQRT_ADD3_ASM
-    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(sb - 1), "v"(pdn), "v"(pup));
-#else
-    r = (sb - 1) + pdn + pup;           // v_add3_u32 from the selector
-#endif
-#endif
-    return __builtin_bit_cast(float, r);
-#else
-    const float t = __builtin_bit_cast(float, edn) <= 0.0f ? dn : s;
-    return __builtin_bit_cast(float, eup) > 0.0f ? up : t;
-#endif
+    return __builtin_bit_cast(float, (sb - 1) + pdn + pup);     // v_add3_u32 from the selector
 }
 
 // min / max of two doubles as single instructions.  In IEEE mode the
@@ -235,12 +152,6 @@ __device__ __forceinline__ double sqrt_normal_f64(double x)
     return __builtin_fma(d, h, g);
 }
 
-#ifndef MCEIK_F64_NOCLAMP
-#define MCEIK_F64_NOCLAMP 0      // 1: drop the 3D root clamp (measured 1.1% slower, profiles/r04_ncl)
-#endif
-#ifndef MCEIK_F64_NOBRANCH
-#define MCEIK_F64_NOBRANCH 0     // 1: the fast fp64 update as straight-line code (A/B)
-#endif
 // The literal fp64 update for the fast path (no ierr): godunov_sel's values
 // with the sort and the minima as bare v_min_f64 / v_max_f64, the 2D root
 // computed unconditionally and no early return (no divergent branch: the
@@ -265,26 +176,7 @@ __device__ __forceinline__ double godunov_fast64(double a, double b, double c, d
     // (a1 == UN needs no test of its own: then a2 = UN too, x1 = UN + f rounds
     // to UN and the 1D case returns it -- the reference's early return)
     const bool r1 = !(x1 > a2), r2 = !(x2 > a3);
-#if MCEIK_F64_NOBRANCH
-    // the choice as masks on the bit patterns: no ternary for the optimiser to
-    // turn into exec-masked branches (with the 2D / 3D arithmetic sunk into
-    // them); instcombine folds each mask pair back into one select
-    const unsigned long long m1 = 0ull - (unsigned long long)r1, m2 = 0ull - (unsigned long long)r2;
-    const unsigned long long b3 = __builtin_bit_cast(unsigned long long, dmin_(x3, UN));
-    const unsigned long long b23 = (__builtin_bit_cast(unsigned long long, x2) & m2) | (b3 & ~m2);
-    return __builtin_bit_cast(double, (__builtin_bit_cast(unsigned long long, x1) & m1) | (b23 & ~m1));
-#elif MCEIK_F64_NOCLAMP
-    // The reference clamps the 3D root at u_nan.  The 3D case is selected
-    // only when x1 > a2 and x2 > a3: with a2 = u_nan x1 = a1 + f cannot exceed
-    // it (a1 + f rounds to u_nan at most), with a3 = u_nan the 2D root cannot
-    // (it is a1-based, finite or x1), so a1..a3 are travel times, all finite
-    // and far below u_nan / 4, and x3 = (-qb + sqrt(disc)) / 2 is too: the
-    // clamp never acts on a selected value.  Dropping it drops the u_nan
-    // constant (an SGPR pair the kernel spills) from the node update.
-    return r1 ? x1 : r2 ? x2 : x3;
-#else
     return r1 ? x1 : r2 ? x2 : (x3 < UN ? x3 : UN);
-#endif
 }
 
 // Branchless fp32 Godunov update, values and ierr identical to the twin
@@ -320,7 +212,7 @@ __device__ __forceinline__ float godunov_bl(float a, float b, float c, float f, 
 template <bool FAST>
 __device__ __forceinline__ double godunov_bl(double a, double b, double c, double f, int &ierr)
 {
-    return MCEIK_F64_SELECT ? godunov_sel(a, b, c, f, ierr) : godunov(a, b, c, f, ierr);   // fp64: literal form
+    return godunov_sel(a, b, c, f, ierr);   // fp64: the literal form's values without its branches
 }
 
 // min of two travel times.  Values in the field are never NaN or -0 (every

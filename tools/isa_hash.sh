@@ -11,7 +11,9 @@ T=$(mktemp -d /tmp/isa_XXXX)
 for f in fsm_kernel fsm16_kernel fsm_single mcmc_kernels capi comm; do
   ( /opt/rocm/bin/hipcc $FLAGS "$@" --cuda-device-only -S csrc/$f.hip -o "$T/$f.s" 2>/dev/null
     # drop the compiler's ident/path lines, keep the ISA and kernel metadata
-    grep -v -E '^\s*\.(ident|file)\b' "$T/$f.s" | sha256sum | sed "s|-|$f|" ) &
+    # and the per-translation-unit id (__hip_cuid_<hash of the path and source>)
+    grep -v -E '^\s*\.(ident|file)\b' "$T/$f.s" | sed -E 's/__hip_cuid_[0-9a-f]+/__hip_cuid/g' | sha256sum |
+        sed "s|-|$f|" ) &
 done
 wait
 rm -rf "$T"
