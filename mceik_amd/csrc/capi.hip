@@ -213,12 +213,15 @@ static WsLayout ws_layout(const mceik_fsm_batch *b)
     size_t es = is_double ? 8 : 4;
     WsLayout w;
     w.nwaves = batch_waves(L, is_double);
+    // the held stream's per-wave z-face copies: read only by the 16-z kernel (the 8-z / fp64
+    // instances read the z-boundary nodes from the field)
+    const size_t zfw = fsm_launch_kind(L, is_double) == 16 ? zf_bytes(L, es) : 0;
     // Every resident wave owns a u and a u0 scratch field: cap the waves so the
     // scratch stays within a fixed budget (deterministic across calls; 256^3
     // fp32 fields are 67 MB, 2048 waves would need 275 GB).  Waves then take
     // several solves each from the queue.
     {
-        const size_t per_wave = 2 * L.field_elems * es + zf_bytes(L, es);
+        const size_t per_wave = 2 * L.field_elems * es + zfw;
         const long cap = (long)(ws_budget_bytes() / (per_wave ? per_wave : 1));
         if (cap >= 1 && w.nwaves > cap) w.nwaves = (int)cap;
     }
@@ -229,7 +232,7 @@ static WsLayout ws_layout(const mceik_fsm_batch *b)
     size_t nu = b->u_out ? (size_t)L.nsolve : (size_t)w.nwaves;
     w.u0 = w.u + nu * L.field_elems * es;
     w.zf = w.u0 + (size_t)w.nwaves * L.field_elems * es;          // the held stream's z-face copies
-    w.total = w.zf + (size_t)w.nwaves * zf_bytes(L, es);
+    w.total = w.zf + (size_t)w.nwaves * zfw;
     return w;
 }
 
@@ -310,6 +313,13 @@ static int fsm_batch_solve_impl(const mceik_fsm_batch *b, void *workspace, size_
         if (fsm_launch_lds_bytes(G, b->precision == 64) > MCEIK_MAX_LDS) {
             fprintf(stderr, "mceik_fsm_batch_solve: %d x %d x %d z-blocks exceed the LDS block tables\n", G.ntx, G.nty,
                     G.nzk);
+            return 1;
+        }
+        // the held stream's 16-bit sweep clocks (fsm_hold.h hold_clock_bound)
+        const bool held = fsm_launch_kind(G, b->precision == 64) == 16 || fsm_compact_layout(G, 8);
+        const int infl = fsm_launch_kind(G, b->precision == 64) == 16 ? fsm16_geo(G).infl : G.infl;
+        if (held && hold_clock_bound(G.nblocks, infl) >= 65536) {
+            fprintf(stderr, "mceik_fsm_batch_solve: %d z-blocks overflow the held stream's 16-bit clocks\n", G.nblocks);
             return 1;
         }
     }

@@ -154,12 +154,10 @@ extern "C" int mceik_mcmc_gather(mceik_mcmc *s, mceik_comm *c, int which, int nc
         fprintf(stderr, "mceik_mcmc_gather: sampler on device %d, communicator on %d\n", sh.device, c->device);
         status = 1;
     }
-    // A checkpoint is synchronous: the sampler's queued steps finish first, then
-    // the gather runs on the communicator's own stream with blocking host copies.
-    if (!status && hipStreamSynchronize((hipStream_t)sh.stream) != hipSuccess) {
-        fprintf(stderr, "mceik_mcmc_gather: the sampler's stream failed\n");
-        status = -1;
-    }
+    // A checkpoint is synchronous: the sampler's queued steps have finished
+    // (mcmc_shard_view synchronised its stream and checked the work queue),
+    // and the gather runs on the communicator's own stream with blocking host
+    // copies.
     const size_t ncell = (size_t)sh.ncell;
     const size_t vbytes = (size_t)nchains_total * ncell * sizeof(int), lbytes = (size_t)nchains_total * sizeof(double);
     // root: receive straight into caller device memory on this GPU, else into a

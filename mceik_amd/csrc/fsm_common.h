@@ -275,6 +275,22 @@ static inline size_t fsm16_lds_bytes(const FsmLaunch &L)
     return fsm16_smem_layout(L, off);
 }
 
+// The held stream (fsm_hold.h) keeps 16-bit clocks relative to the sweep: a
+// sweep needs at most nblocks (1 + infl) + 64 of them (between two visits at
+// most infl bubbles).
+// The bound at the tables' capacity and the largest infl of either kernel:
+// the 16-z kernel's at kb16 = 2 (its smallest z-block) and the 8-z compact
+// instances' at kb = MCEIK_KB (fsm16_geo / fsm_geometry).  The host checks
+// every launch as well (mceik_fsm_batch_solve).
+static inline __host__ __device__ constexpr int hold_clock_bound(int nblocks, int infl)
+{
+    return nblocks * (1 + infl) + 64;
+}
+static_assert(hold_clock_bound(MCEIK_MAX_BLOCKS, 1 + (14 + MCEIK_AHEAD16 + 1) / 2) < 65536,
+              "16-bit held-stream clocks: MCEIK_MAX_BLOCKS / MCEIK_AHEAD16 too large");
+static_assert(hold_clock_bound(MCEIK_MAX_BLOCKS, 1 + (14 + MCEIK_AHEAD + MCEIK_KB - 1) / MCEIK_KB) < 65536,
+              "16-bit held-stream clocks: MCEIK_MAX_BLOCKS / MCEIK_AHEAD too large");
+
 // Fills the tile geometry of a launch from nx, ny, nz (es: element bytes).
 // Field layout: per 8x8 column tile, z-major groups of one
 // 128-B line per column (32 fp32 / 16 fp64 z values), columns in colpos order.

@@ -215,7 +215,7 @@ __device__ __forceinline__ void hold_settle(const FsmLaunch &L, const HoldLds<Or
 // Start of a sweep: every block's pending state (need >= lastproc) becomes
 // need 1 / 0 against lastproc 1, the frontiers restart, and the sweep's clock
 // starts at 64 (a sweep needs at most nblocks (1 + infl) + 64 < 2^16 clocks:
-// between two visits at most infl bubbles).
+// between two visits at most infl bubbles; fsm_common.h hold_clock_bound).
 template <typename OrderT>
 __device__ __forceinline__ void hold_norm(const FsmLaunch &L, const HoldLds<OrderT> &H)
 {
