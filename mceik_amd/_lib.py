@@ -92,6 +92,7 @@ EXPORTS = ("eikonal3d_serial_driver", "eikonal3d_serial_driver_sp", "eikonal3d_b
            "eikonal3d_finalize", "locate3d_gridsearch__double64", "locate3d_gridsearch__float64",
            "locate_l2_gridSearch__double64",
            "locate_l2_gridSearch__float64", "mceik_relocate",
+           "locate3d_initialize", "locate3d_gridsearch", "locate3d_finalize",
            "mceik_fsm_workspace_bytes", "mceik_fsm_batch_solve", "mceik_fsm_bytes_per_node_sweep", "mceik_fsm_step_z",
            "mceik_fsm_kernel_name", "mceik_fsm_lds_bytes",
            "mceik_memcpy",

@@ -83,6 +83,10 @@ void mpiutils_getCommunicators(int *globalComm, int *intraTableComm, int *interT
     *ierr = 0;
 }
 
+/* whether mpiutils_initialize3d has split the communicators (locate3d.hip:
+ * the reference's linitComm, locate.f90:610) */
+__attribute__((visibility("hidden"))) int mceik_mpiutils_initialized(void) { return g_comm.init; }
+
 void mpiutils_finalize(void)
 {
     if (!g_comm.init) return;

@@ -9,9 +9,15 @@
  * builds them (homog.c:90-110) -- then
  * eikonal_h5io_initLocations, a logJPDF write / read, readModel,
  * getModelDimensions and finalize.  Exit 0 when every check passes.
+ * With a fourth argument "locate <job>" it also runs homog.c:428-450's
+ * location step on the tables it wrote (locate3d_initialize / gridsearch /
+ * finalize, include/locate.h) and rank 0 prints every hypocentre and the
+ * estimates of event 1 ("LOCATE ...", "TEST ..." lines, %.17g); picks whose
+ * table was not written (station 3's S picks) are not used.
  *
- *   mpiexec -n {1,2,4} homog_h5io <dir> <proj> [ndivx]   (ndivx blocks per table: nprocs / ndivx
- *   table groups, each writing <proj>_<group>_ttimes.h5 through its intra-table communicator)
+ *   mpiexec -n {1,2,4} homog_h5io <dir> <proj> [ndivx [locate <job>]]   (ndivx blocks per table:
+ *   nprocs / ndivx table groups, each writing <proj>_<group>_ttimes.h5 through its intra-table
+ *   communicator)
  */
 #include <math.h>
 #include <stdio.h>
@@ -21,6 +27,7 @@
 #include <mpi.h>
 
 #include "h5io.h"
+#include "locate.h"
 #include "mceik_broadcast.h"
 #include "mceik_struct.h"
 #include "mpiutils.h"
@@ -201,6 +208,31 @@ int main(int argc, char **argv)
     for (size_t i = 0; i < nloc; i++) t4[i] = -(float)(i % 97) - 0.25f * (float)myblock;
     CHECK(eikonal_h5io_writeLocationLogJPDF(MPI_COMM_WORLD, lfid, model, 2, ix0, iy0, iz0, nxL, nyL, nzL, t4) == 0,
           "writeLocationLogJPDF");
+    if (argc > 5 && !strcmp(argv[4], "locate")) {   /* homog.c:428-450 */
+        const int locJob = atoi(argv[5]);
+        int iverb = 0;
+        long tl = (long)tfid, ll = (long)lfid;
+        locate3d_initialize(&intra, &iverb, &tl, &ll, &ndivx, &ndivy, &ndivz, &ierr);
+        CHECK(ierr == 0, "locate3d_initialize");
+        double *hypo = calloc((size_t)cat.nevents * 4, sizeof(double));
+        int nobs = 2 * st.nstat;
+        double *statCor = calloc((size_t)nobs, sizeof(double));
+        for (int i = 0; i < cat.nevents; i++) cat.tori[i] = 0.5 * i;        /* job 1's fixed origin times */
+        for (int i = 0; i < cat.nevents * nobs; i++)
+            if (cat.pickType[i] == S_PRIMARY_PICK && !st.lhasS[cat.statPtr[i] - 1]) cat.luseObs[i] = 0;
+        locate3d_gridsearch(&model, &locJob, &nobs, &cat.nevents, cat.luseObs, cat.statPtr, cat.pickType, statCor,
+                            cat.tori, cat.varObs, cat.tobs, cat.test, hypo, &ierr);
+        CHECK(ierr == 0, "locate3d_gridsearch");
+        locate3d_finalize();
+        if (myid == 0) {
+            for (int i = 0; i < cat.nevents; i++)
+                printf("LOCATE %d %.17g %.17g %.17g %.17g\n", i + 1, hypo[4 * i], hypo[4 * i + 1], hypo[4 * i + 2],
+                       hypo[4 * i + 3]);
+            for (int i = 0; i < nobs; i++) printf("TEST %d %d %.17g\n", i + 1, cat.luseObs[i], cat.test[i]);
+        }
+        free(hypo);
+        free(statCor);
+    }
     CHECK(eikonal_h5io_finalize(intraComm, &tfid) == 0 && eikonal_h5io_finalize(intraComm, &lfid) == 0,
           "finalize");
     mpiutils_finalize();

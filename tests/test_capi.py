@@ -16,7 +16,7 @@ REF_INC = "/root/reference/include"
 
 def _declared_functions():
     names = set()
-    for h in ("mceik.h", "mceik_eikonal.h", "os.h"):
+    for h in ("mceik.h", "mceik_eikonal.h", "os.h", "locate.h"):
         txt = open(os.path.join(INC, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         for m in re.finditer(r"^\s*(?:int|void|size_t|double|bool|const char)\s+\**\s*([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
@@ -164,3 +164,18 @@ def test_c_callers_compile_and_link(tmp_path, src, mpi):
     cmd += [f"-Wl,-rpath,/usr/lib/x86_64-linux-gnu:{lib}" + (f":{mpidir}/lib" if mpi else ""), "-lm",
             "-o", str(tmp_path / "caller")]
     subprocess.run(cmd, check=True)
+
+
+def test_locate3d_refuses_before_initialize_and_unknown_jobs():
+    """include/locate.h (locate.f90:322-519): locate3d_gridsearch without a
+    locate3d_initialize, and the jobs the reference leaves "not yet done" (3,
+    5) or rejects, return ierr 1 before any GPU work (CPU host)."""
+    import ctypes as C
+    from mceik_amd import _lib
+    L = _lib.lib()
+    i = lambda v: C.byref(C.c_int(v))
+    ierr = C.c_int(0)
+    z = C.c_void_p(0)
+    L.locate3d_finalize()
+    L.locate3d_gridsearch(i(1), i(2), i(0), i(0), z, z, z, z, z, z, z, z, z, C.byref(ierr))
+    assert ierr.value == 1
