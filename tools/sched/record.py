@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-ZB = 32          # z per z-block (kb = 4 bricks of 8 z)
+ZB = int(os.environ.get("MCEIK_SIM_ZB", "32"))   # z per z-block (kb = 4 bricks of 8 z; 64: 4-step positions)
 
 
 def block_flags(diff, nx, ny, nz):
@@ -182,7 +182,7 @@ def main():
     import multiprocessing as mp
     with mp.get_context("fork").Pool(a.workers) as pool:
         res = pool.map(record_one, jobs)
-    out = {"stations": np.array(st), "nx": p.nx, "ny": p.ny, "nz": p.nz}
+    out = {"stations": np.array(st), "nx": p.nx, "ny": p.ny, "nz": p.nz, "zb": ZB}
     for k_, (c, f, bc, it, orl, frl) in enumerate(res):
         out[f"chg{k_}"], out[f"face{k_}"], out[f"bc{k_}"], out[f"niter{k_}"] = c, f, bc, it
         if a.rel is not None:

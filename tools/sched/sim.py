@@ -387,7 +387,7 @@ def main():
     LEVEL = a.level
     FORCEK = a.forcek
     R = np.load(a.rec)
-    g = Geo(int(R["nx"]), int(R["ny"]), int(R["nz"]))
+    g = Geo(int(R["nx"]), int(R["ny"]), int(R["nz"]), zb=int(R["zb"]) if "zb" in R else 32)
     nst = len(R["stations"])
     agg = {}
     for pol in a.policies.split(","):
