@@ -888,6 +888,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             TRAF(S, 0, b3.seg != OOB, 64);
             TRAF(S, 2, b3.zh != OOB, 4);
         }
+        __builtin_amdgcn_s_setprio(0);               // the update at the SIMD's low priority (below)
         // ---- u0: old values of a block's first visit in the iteration (< T only); none once the
         // iteration is known unconverged (the verify that reads them does not run)
         const bool wnc = !__any(notconv);
@@ -918,6 +919,12 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         changed = changed && val;
         notconv |= nc && val;
         nchg += changed ? 2u : 0u;                   // in 8-z segment equivalents
+        // From here to the next step's loads the wave issues at raised priority:
+        // its bookkeeping (load waits, row writes, stores, the stream decision and
+        // the next prefetch) is a chain of dependent short instructions, and the
+        // other wave of the SIMD, inside its update, fills the cycles in between
+        // (+0.7%, profiles/r06_prio2).
+        __builtin_amdgcn_s_setprio(2);
 
         // ---- consume this step's loads before any store of the step
         if (cc_pend >= 0) cc_write<float, CCR>(L, S.cc, cc_pend, ccv, ccsize, (float)L.h);
@@ -1005,6 +1012,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             } while (step(Par16<0>()));
         }
     }
+    __builtin_amdgcn_s_setprio(0);
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     // the last visits' changes (every lane is past them)
     for (int q = max(0, nstream - g.infl + 1); q < nstream; q++) hold_settle(L, H, q % nr, clock0 + q);

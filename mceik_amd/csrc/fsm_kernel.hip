@@ -871,6 +871,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
 
         // ---- the 8 z-slots of the current brick (held stream: a run end's z-downwind node is the
         // one loaded from HBM)
+        __builtin_amdgcn_s_setprio(0);          // the update at the SIMD's low priority (fsm16_kernel.hip)
         bool changed = false, nc = false, c0 = false, c7 = false;
         const bool zdsel = HOLD && b0.zd && !(S.fmask[b0.ri] & HOLD_CONT);
         if (__any(b0.fl & F_SLOW))
@@ -886,6 +887,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         changed = changed && val;
         notconv |= nc && val;
         nchg += changed ? 1u : 0u;
+        __builtin_amdgcn_s_setprio(2);          // the bookkeeping to the next loads at raised priority
 
         // ---- consume this step's loads before any store of the step is issued.
         // gfx9's vmcnt retires loads and stores in issue order, so a wait for a
@@ -995,6 +997,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         do {
         } while (step(c, n, hq, hn));
     }
+    __builtin_amdgcn_s_setprio(0);
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     if constexpr (HOLD) {
         // the last visits' changes (every lane is past them)
