@@ -39,6 +39,29 @@ __device__ __forceinline__ uint32_t zoff16(int zb)
     return ((u >> 1) << 13) | ((u & 1u) << 6);
 }
 
+// Phase clocks (MCEIK_PHASECLK instrumentation builds, with MCEIK_TRAFFIC for
+// the counters' plumbing): shader-clock cycles of a step's phases, summed per
+// wave into the traffic categories 0..6 in place of bytes -- 0 prefetch issue,
+// 1 u0 copies, 2 brick update, 3 load waits / row writes / stores, 4 stream
+// decision (fsm_hold.h hold_decide), 5 its admission (ring, column meta, cell
+// cache loads), 6 the sweep outside its step loop; 7 counts hold_decide's
+// window rounds.  The clock reads wait for the
+// wave's outstanding LDS and scalar loads, so phases are slightly serialised.
+#ifdef MCEIK_PHASECLK
+#undef TRAF
+#undef TRAFU
+#define TRAF(S, k, pred, bytes) do { } while (0)
+#define TRAFU(S, k, bytes) do { } while (0)
+#define PCLK(k)                                                                                         \
+    do {                                                                                                \
+        const unsigned long long t_ = __builtin_readcyclecounter();                                     \
+        if (threadIdx.x == 0) S.scratch[8 + (k)] += (int)(t_ - pclk_t);                                 \
+        pclk_t = t_;                                                                                    \
+    } while (0)
+#else
+#define PCLK(k) do { } while (0)
+#endif
+
 // ---- LDS ------------------------------------------------------------------
 struct Smem16 {
     int *box;                    // BC boxes [nsrc][6]
@@ -490,12 +513,13 @@ __device__ __forceinline__ HoldLds<unsigned short> hold_lds16(const Smem16 &S)
 
 // Admit position (ring slot ri, relative clock C): every lane writes its
 // column meta, lane 0 the ring entry, block id, tile base and the block's
-// visit clock.  u0 flag: the block's first visit in this iteration (the
-// held stream's visited bitmap).
+// visit clock.  u0flag: the block's first visit in this iteration (no visit
+// since the iteration started: the held stream's clocks restart every sweep,
+// so the iteration's visits are a bitmap, read by hold_decide).
 template <bool RZ, bool LEAN>
 __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, const Smem16 &S, const BcBoxes &bc,
-                                        int entry, int zh, int ri, int C, int lx, int ly, int lxs, int lys, int rx,
-                                        int ry, ColTile &ct)
+                                        int entry, int zh, int u0flag, int ri, int C, int lx, int ly, int lxs,
+                                        int lys, int rx, int ry, ColTile &ct)
 {
     unsigned meta = 0;
     int bid = 0, nbv = 0;
@@ -504,9 +528,6 @@ __device__ __forceinline__ void admit16(const FsmLaunch &L, const Fsm16Geo &g, c
         const int tz = (entry >> 24) & 0xff, tx = entry & 0xfff, ty = (entry >> 12) & 0xfff;
         bid = tz * L.ntiles + tx + ty * L.ntx;
         nbv = min(L.kb, L.nzb - tz * L.kb);          // 8-z bricks of the block (visit statistics)
-        // no visit since the iteration started (the held stream's clocks restart every sweep, so the
-        // iteration's visits are a bitmap)
-        const int u0flag = !((S.vbits[bid >> 5] >> (bid & 31)) & 1u);
         if ((entry & 0xffffff) != ct.tile) column_tile<float>(L, bc, entry, lx, ly, lxs, lys, rx, ry, ct);
         meta = LEAN ? lean_word<RZ>(L, g, ct, tz, ri, u0flag, zh) : column_word(L, L.kb, ct, tz, ri, u0flag, zh);
         base = (uint32_t)(ty * L.ntx + tx) * tile_bytes<float>(L) + (LEAN ? (uint32_t)tz << 13 : 0u);
@@ -637,6 +658,9 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
                                        int &ierr_last, unsigned &nchg, unsigned &nsteps)
 {
     const Rsrc zr_ = zfr;                            // the z-boundary nodes: the z-face copies
+#ifdef MCEIK_PHASECLK
+    unsigned long long pclk_t = __builtin_readcyclecounter();
+#endif
     const int lane = threadIdx.x, lxs = lane & 7, lys = lane >> 3, d = lxs + lys;
     const int lx = rx ? 7 - lxs : lxs, ly = ry ? 7 - lys : lys;
     const float UN = FLT_MAX;
@@ -652,8 +676,8 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     const uint32_t hcol = (uint32_t)colpos(hlx, hly) * 128u;
 
     const HoldLds<unsigned short> H = hold_lds16(S);
-    // (the held stream's scan state -- first incomplete tile, previous position's tile -- lives in LDS
-    // scratch [4], [5]: fewer scalar registers live across the step loop)
+    // (the held stream's scan state -- first incomplete tile, previous position's tile and its cached
+    // status inputs -- lives in LDS scratch [4..6]: fewer scalar registers live across the step loop)
     // this lane's change-mask bits of a changed brick: the block, and its x / y faces when the
     // lane's column is a tile edge (absolute orientation)
     const unsigned xyface = HOLD_OWN | (lx == 0 ? 2u : 0u) | (lx == 7 ? 4u : 0u) | (ly == 0 ? 8u : 0u) |
@@ -662,12 +686,13 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     if (lane == 0) { S.scratch[4] = 0; S.scratch[5] = -1; }
     clock0 = 64;
     // the next position's block (after settling the visit infl positions back)
-    auto decide_any = [&](int pos, int ri, int &zh) __attribute__((always_inline)) -> int {
+    auto decide_any = [&](int pos, int ri, int &zh, int &u0) __attribute__((always_inline)) -> int {
         // positions are decided one after another: settle the one infl back
+        const HoldSt hs = hold_state(S.scratch + 4);
         const int q = pos - g.infl;
         if (q >= 0) hold_settle(L, H, q % nr, clock0 + q);
-        return hold_decide<RZ>(L, H, S.scratch + 4, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, g.infl, g.vis,
-                               zh);
+        return hold_decide<RZ>(L, H, S.scratch + 4, hs, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, g.infl,
+                               g.vis, zh, u0);
     };
     constexpr bool FL = KB16 == 2;                   // full-line own loads (2-step positions)
     constexpr bool LEAN = KB16 == 2;                 // lean position words (2-step positions)
@@ -700,14 +725,14 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     constexpr int AH = MCEIK_AHEAD16;
     int ndecided = 0, nstream = 0x7fffffff, dri = 0;
     for (int pos = 0; pos <= (AH - 1) / kb; pos++) {
-        int zh;
-        const int e = decide_any(pos, dri, zh);
+        int zh, u0;
+        const int e = decide_any(pos, dri, zh, u0);
         if (e == -2) {
             if (pos == 0) return 0;                         // nothing changed near any block: skip the sweep
             nstream = pos;
             break;
         }
-        admit16<RZ, LEAN>(L, g, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
+        admit16<RZ, LEAN>(L, g, S, bc, e, zh, u0, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
         if (e >= 0) {
             cc_issue<CCR>(L, L.kb, sr, e, ccv, ccsize);
             TRAFU(S, 5, ccsize * 4);
@@ -829,12 +854,13 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         ccri = 0;
         if (ph == 0 && nstream == 0x7fffffff) {
             const int pos = ndecided;
-            int zh;
-            const int e = decide_any(pos, dri, zh);
+            int zh, u0;
+            const int e = decide_any(pos, dri, zh, u0);
+            PCLK(4);
             if (e == -2) {
                 nstream = pos;
             } else {
-                admit16<RZ, LEAN>(L, g, S, bc, e, zh, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
+                admit16<RZ, LEAN>(L, g, S, bc, e, zh, u0, dri, clock0 + pos, lx, ly, lxs, lys, rx, ry, ct);
                 if (e >= 0) {
                     cc_issue<CCR>(L, L.kb, sr, e, ccv, ccsize);
                     TRAFU(S, 5, ccsize * 4);
@@ -888,6 +914,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
             TRAF(S, 0, b3.seg != OOB, 64);
             TRAF(S, 2, b3.zh != OOB, 4);
         }
+        PCLK(0);
         __builtin_amdgcn_s_setprio(0);               // the update at the SIMD's low priority (below)
         // ---- u0: old values of a block's first visit in the iteration (< T only); none once the
         // iteration is known unconverged (the verify that reads them does not run)
@@ -908,6 +935,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         const unsigned fmk = S.fmask[b0.ri()];
         if ((b0.w1 & W1_ZD) && !(fmk & HOLD_CONT)) znext = zc;
         const float zp0 = (b0.fl() & F_ZH) ? zc : zprev;
+        PCLK(1);
         bool changed = false, nc = false, c0 = false, c15 = false;
         if (__any(b0.fl() & F_SLOW))
             brick16<RZ, true, LEAN>(L, S, b0, v, zp0, znext, lx, ly, rx, ry, changed, nc, ierr_last, c0, c15);
@@ -924,6 +952,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         // the next prefetch) is a chain of dependent short instructions, and the
         // other wave of the SIMD, inside its update, fills the cycles in between
         // (+0.7%, profiles/r06_prio2).
+        PCLK(2);
         __builtin_amdgcn_s_setprio(2);
 
         // ---- consume this step's loads before any store of the step
@@ -998,10 +1027,13 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
         b1 = b3;
         if (++ph == kb) ph = 0;
         B++;
+        PCLK(3);
         decide_step();
+        PCLK(5);
         return more();
     };
     decide_step();
+    PCLK(6);
     if (more()) {
         if (FL) {
             do {
@@ -1016,6 +1048,7 @@ __device__ __forceinline__ int sweep16(const FsmLaunch &L, const Fsm16Geo &g, Rs
     nsteps += (unsigned)B;                           // macro steps of this sweep (visit statistics)
     // the last visits' changes (every lane is past them)
     for (int q = max(0, nstream - g.infl + 1); q < nstream; q++) hold_settle(L, H, q % nr, clock0 + q);
+    PCLK(6);
     return nstream;
 }
 

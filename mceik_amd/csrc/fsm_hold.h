@@ -66,6 +66,168 @@ __device__ __forceinline__ void hold_txy(const HoldLds<OrderT> &H, int ti, int &
     txs = o & ((1 << SH) - 1);
     tys = o >> SH;
 }
+// The next undecided block (sweep-z index k) of tile id at clock C, its upwind
+// x / y tiles xu / yu (-1: none): HOLD_DONE (k >= nzk) / BLOCKED (an upwind
+// tile has not decided that far) / HELD / WAIT (a reason, but an upwind visit
+// is < vis back) / SKIP / READY; runon: its z-below is the previous position.
+// Every read is issued up front (absent neighbours and a DONE tile read the
+// tile's own entries, unused): one LDS round trip per call.  u0: the block
+// has not been visited in this iteration (the admission's u0 flag).
+template <bool RZ, typename OrderT>
+__device__ __forceinline__ int hold_status(const FsmLaunch &L, const HoldLds<OrderT> &H, int id, int xu, int yu, int k,
+                                           int C, int infl, int vis, int &runon, int &u0)
+{
+    const int nt = L.ntiles, nzk = L.nzk;
+    const int kc = min(k, nzk - 1);
+    const int tz = RZ ? nzk - 1 - kc : kc;
+    const int b = tz * nt + id;
+    int fxu = H.fz[xu >= 0 ? xu : id], fyu = H.fz[yu >= 0 ? yu : id];
+    int nb = H.need[b], lb = H.lastproc[b];
+    int lxu = H.lastproc[tz * nt + (xu >= 0 ? xu : id)], lyu = H.lastproc[tz * nt + (yu >= 0 ? yu : id)];
+    int lzl = H.lastproc[kc > 0 ? b + (RZ ? nt : -nt) : b];
+    unsigned vw = H.vbits[b >> 5];
+    asm volatile("" : "+v"(fxu), "+v"(fyu), "+v"(nb), "+v"(lb), "+v"(lxu), "+v"(lyu), "+v"(lzl), "+v"(vw));
+    u0 = !((vw >> (b & 31)) & 1u);                       // no visit of the block in this iteration yet
+    runon = 0;
+    if (k >= nzk) return HOLD_DONE;
+    if ((xu >= 0 && fxu <= k) || (yu >= 0 && fyu <= k)) return HOLD_BLOCKED;
+    const bool reason = nb >= lb;
+    int dep = -0x40000000;                               // latest upwind visit (this sweep's clocks)
+    if (xu >= 0) dep = max(dep, lxu);
+    if (yu >= 0) dep = max(dep, lyu);
+    const int zl = k > 0 ? lzl : -0x40000000;
+    runon = zl == C - 1;
+    if (!runon) dep = max(dep, zl);
+    if (reason) return dep + vis <= C ? HOLD_READY : HOLD_WAIT;
+    return (runon || dep > C - infl) ? HOLD_HELD : HOLD_SKIP;
+}
+// The scan state a decision starts from (LDS sst[0..2]): [0] tiles [0, done)
+// of the diagonal order are complete, [1] diagonal index of the previous
+// position's tile (-1 none), [2] that tile's id | its next sweep-z index << 16
+// | upwind x / y tile flags << 24.  Read before the same decision's settle, so
+// the two round trips overlap (values per lane; hold_decide makes them scalar).
+struct HoldSt {
+    int done, last, lc;
+};
+__device__ __forceinline__ HoldSt hold_state(const int *sst)
+{
+    asm volatile("" ::: "memory");
+    return HoldSt{sst[0], sst[1], sst[2]};
+}
+// The block of position C (the previous position's ring slot rprev): the next
+// block of the previous position's tile when it is ready, else the first ready
+// block in diagonal order -- windows of 64 tiles from the first incomplete one,
+// every lane deciding its tile's next block per round, until a block is ready
+// or no lane can skip.  Returns the entry tx | ty << 12 | tz << 24, -1 (a
+// bubble) or -2 (every tile decided: the sweep's stream ends); zh: a run start
+// above the column's first block (its z-upwind node comes from HBM).
+// Progress: the first incomplete tile's upwind tiles are complete, so within
+// infl positions its next block is ready or skipped.
+// Round trips: the previous tile's status from the cached state (one); the
+// front scan (tile order, frontiers: two), whose window the first round reuses
+// when the front did not move; one per round (a lane's own frontier is
+// tracked in registers: only its lane advances it within a window).
+template <bool RZ, typename OrderT>
+__device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<OrderT> &H, int *sst, const HoldSt &sr,
+                                           int C, int rx, int ry, int rprev, int infl, int vis, int &zh, int &u0)
+{
+    const int lane = threadIdx.x, nt = L.ntiles, nzk = L.nzk;
+    const int dxu = rx ? 1 : -1, dyu = ry ? L.ntx : -L.ntx;
+    zh = 0;
+    u0 = 0;
+    int pick = -1, pid = 0, pk = 0, pro = 0, pfl = 0, pu0 = 0;
+    int done = __builtin_amdgcn_readfirstlane(sr.done);
+    const int last = __builtin_amdgcn_readfirstlane(sr.last), lc = __builtin_amdgcn_readfirstlane(sr.lc);
+    if (last >= 0) {
+        const int id = lc & 0xffff, k = (lc >> 16) & 0xff, fl = (lc >> 24) & 3;
+        int ro, v0;
+        const int s = hold_status<RZ>(L, H, id, (fl & 1) ? id + dxu : -1, (fl & 2) ? id + dyu : -1, k, C, infl, vis,
+                                      ro, v0);
+        if (__builtin_amdgcn_readfirstlane(s) == HOLD_READY) {
+            pick = last;
+            pid = id;
+            pk = k;
+            pro = __builtin_amdgcn_readfirstlane(ro);
+            pu0 = __builtin_amdgcn_readfirstlane(v0);
+            pfl = fl;
+        }
+    }
+    if (pick < 0) {
+        // this lane's tile of the window at wbase: id, upwind tiles, frontier (255: none)
+        int wbase = -1, ti = 0, id = 0, xu = -1, yu = -1, k = 255;
+        auto window = [&](int base) __attribute__((always_inline)) {
+            wbase = base;
+            ti = base + lane;
+            const bool in = ti < nt;
+            int txs, tys;
+            hold_txy(H, in ? ti : 0, txs, tys);
+            const int tx = rx ? L.ntx - 1 - txs : txs, ty = ry ? L.nty - 1 - tys : tys;
+            id = ty * L.ntx + tx;
+            xu = txs > 0 ? id + dxu : -1;
+            yu = tys > 0 ? id + dyu : -1;
+            const int f = H.fz[id];
+            k = in ? f : 255;
+        };
+        for (;;) {                                   // the complete tiles at the front
+            window(done);
+            const unsigned long long m = ~__ballot(ti < nt && k >= nzk);
+            const int n = m ? __builtin_ctzll(m) : 64;
+            done += n;
+            if (n < 64) break;
+        }
+        if (done >= nt) {
+            asm volatile("" ::: "memory");
+            if (lane == 0) { sst[0] = done; sst[1] = -1; }
+            asm volatile("" ::: "memory");
+            return -2;
+        }
+        for (int base = done; base < nt && pick < 0; base += 64) {
+            if (base != wbase) window(base);
+            for (;;) {
+#ifdef MCEIK_PHASECLK
+                if (lane == 0) sst[4 + 7] += 1;           // traffic category 7: window rounds
+#endif
+                int ro, v0;
+                const int s0 = hold_status<RZ>(L, H, id, xu, yu, k, C, infl, vis, ro, v0);
+                const int s = ti < nt ? s0 : HOLD_DONE;
+                const bool sk = s == HOLD_SKIP;
+                if (sk) H.fz[id] = (unsigned char)(k + 1);
+                const unsigned long long rm = __ballot(s == HOLD_READY);
+                if (rm) {
+                    const int f = __builtin_ctzll(rm);
+                    pick = base + f;
+                    pid = __builtin_amdgcn_readfirstlane(__shfl(id, f, 64));
+                    pk = __builtin_amdgcn_readfirstlane(__shfl(k, f, 64));
+                    pro = __builtin_amdgcn_readfirstlane(__shfl(ro, f, 64));
+                    pu0 = __builtin_amdgcn_readfirstlane(__shfl(v0, f, 64));
+                    pfl = __builtin_amdgcn_readfirstlane(__shfl((xu >= 0 ? 1 : 0) | (yu >= 0 ? 2 : 0), f, 64));
+                    break;
+                }
+                if (!__ballot(sk)) break;
+                k += sk ? 1 : 0;
+                asm volatile("" ::: "memory");       // this round's frontiers feed the next
+            }
+        }
+    }
+    asm volatile("" ::: "memory");
+    if (pick < 0) {
+        if (lane == 0) { sst[0] = done; sst[1] = -1; }
+        asm volatile("" ::: "memory");
+        return -1;
+    }
+    if (lane == 0) {
+        H.fz[pid] = (unsigned char)(pk + 1);
+        if (pro) atomicOr(&H.fmask[rprev], HOLD_CONT);   // the previous position's run continues here
+        sst[0] = done;
+        sst[1] = pick;
+        sst[2] = pid | ((pk + 1) << 16) | (pfl << 24);
+    }
+    asm volatile("" ::: "memory");
+    zh = pk > 0 && !pro;
+    u0 = pu0;
+    const int ty = pid / L.ntx, tx = pid - ty * L.ntx;
+    return tx | (ty << 12) | ((RZ ? L.nzk - 1 - pk : pk) << 24);
+}
 template <typename OrderT>
 __device__ __forceinline__ int hold_tile_id(const FsmLaunch &L, const HoldLds<OrderT> &H, int ti, int rx, int ry)
 {
@@ -73,12 +235,18 @@ __device__ __forceinline__ int hold_tile_id(const FsmLaunch &L, const HoldLds<Or
     hold_txy(H, ti, txs, tys);
     return (ry ? L.nty - 1 - tys : tys) * L.ntx + (rx ? L.ntx - 1 - txs : txs);
 }
+// ---- the decision as the fp64 instances make it (fsm_kernel.hip) ----------
+// Same decisions as hold_decide below, with the tile geometry read from the
+// order table on every call and no cached state (four LDS round trips for the
+// previous tile's status, two for the front scan, three per window round).
+// The fp64 kernel keeps this form: the round-trip-lean one moved its register
+// allocation and measured 0.7% slower there (profiles/r06_hd).
 // The next undecided block of the tile at diagonal index ti at clock C:
 // HOLD_DONE / BLOCKED (an upwind tile has not decided that far) / HELD / WAIT
 // (a reason, but an upwind visit is < vis back) / SKIP / READY; id, k: the
 // tile and the block's sweep-z index, runon: its z-below is the previous position.
 template <bool RZ, typename OrderT>
-__device__ __forceinline__ int hold_status(const FsmLaunch &L, const HoldLds<OrderT> &H, int ti, int C, int rx, int ry,
+__device__ __forceinline__ int hold_status_scan(const FsmLaunch &L, const HoldLds<OrderT> &H, int ti, int C, int rx, int ry,
                                            int infl, int vis, int &id, int &k, int &runon)
 {
     int txs, tys;
@@ -114,7 +282,7 @@ __device__ __forceinline__ int hold_status(const FsmLaunch &L, const HoldLds<Ord
 // Progress: the first incomplete tile's upwind tiles are complete, so within
 // infl positions its next block is ready or skipped.
 template <bool RZ, typename OrderT>
-__device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<OrderT> &H, int *sst, int C, int rx,
+__device__ __forceinline__ int hold_decide_scan(const FsmLaunch &L, const HoldLds<OrderT> &H, int *sst, int C, int rx,
                                            int ry, int rprev, int infl, int vis, int &zh)
 {
     const int lane = threadIdx.x, nt = L.ntiles;
@@ -124,7 +292,7 @@ __device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<Ord
     struct { int done, last; } st = {__builtin_amdgcn_readfirstlane(sst[0]), __builtin_amdgcn_readfirstlane(sst[1])};
     if (st.last >= 0) {
         int id, k, ro;
-        const int s = hold_status<RZ>(L, H, st.last, C, rx, ry, infl, vis, id, k, ro);
+        const int s = hold_status_scan<RZ>(L, H, st.last, C, rx, ry, infl, vis, id, k, ro);
         if (__builtin_amdgcn_readfirstlane(s) == HOLD_READY) {
             pick = st.last;
             pid = __builtin_amdgcn_readfirstlane(id);
@@ -151,7 +319,7 @@ __device__ __forceinline__ int hold_decide(const FsmLaunch &L, const HoldLds<Ord
             const int ti = base + lane;
             for (;;) {
                 int s = HOLD_DONE, id = 0, k = 0, ro = 0;
-                if (ti < nt) s = hold_status<RZ>(L, H, ti, C, rx, ry, infl, vis, id, k, ro);
+                if (ti < nt) s = hold_status_scan<RZ>(L, H, ti, C, rx, ry, infl, vis, id, k, ro);
                 const bool sk = s == HOLD_SKIP;
                 if (sk) H.fz[id] = (unsigned char)(k + 1);
                 const unsigned long long rm = __ballot(s == HOLD_READY);

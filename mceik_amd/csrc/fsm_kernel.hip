@@ -696,8 +696,8 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
             // positions are decided one after another: settle the one infl back
             const int q = pos - L.infl;
             if (q >= 0) hold_settle(L, H, q % nr, clock0 + q);
-            return hold_decide<RZ>(L, H, S.scratch + 4, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, L.infl,
-                                   L.vis, zh);
+            return hold_decide_scan<RZ>(L, H, S.scratch + 4, clock0 + pos, rx, ry, ri == 0 ? nr - 1 : ri - 1, L.infl,
+                                        L.vis, zh);
         } else {
             return decide<R, RZ>(L, S, st, clock0 + pos, rx, ry, zh);
         }

@@ -19,6 +19,6 @@ if [ "${F_PART:-1}" = 1 ]; then
   echo "[r06_f] bench (driver arguments)"
   timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.log" 2>&1
 else
-  M_OUT=${F_OUT:-r06_f}/m M_PRECS="32 64" M_TRACE=1 M_CONFIGS=1 M_REHEARSAL=0 timeout -k 10 1100 bash tools/measure_r05.sh
+  M_OUT=${F_OUT:-r06_f}/m M_PRECS="${F_PRECS:-32 64}" M_TRACE=1 M_CONFIGS=1 M_REHEARSAL=0 timeout -k 10 1100 bash tools/measure_r05.sh
 fi
 echo done > "$O/DONE"
