@@ -35,7 +35,7 @@ METRIC = "MCMC proposals/sec (FSM eikonal + likelihood), 128³ grid, 1/2/4/8 MI3
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 # sweep-kernel revision per precision (bump when that kernel changes; the
 # profiles/traffic.json record of that precision must match)
-KERNEL_REVS = {32: "fsm-v41", 64: "fsm-v37c"}
+KERNEL_REVS = {32: "fsm-v41", 64: "fsm-v42"}
 
 
 # ---------------------------------------------------------------- CPU baseline

@@ -211,30 +211,47 @@ __device__ __forceinline__ uint32_t halo_offset(const FsmLaunch &L, int kb, cons
 // (7, j - 8)) XN 64 + j - 8, 16..23 (y-upwind of (j - 16, 0)) XR 72 + j - 16,
 // 24..31 (y-downwind of (j - 24, 7)) XN 72 + j - 24.
 #define XROW(arr, half, row) ((((arr) * 2 + (half)) * MCEIK_XROWS + (row)) * 4)
+// Element offsets by precision: xrow = slot 0 of a row, xz(z) = z-slot z (0..7)
+// from there.  fp32: [arr][half][row][4] (XROW, a row's four slots contiguous);
+// fp64: [arr][z][row], so that a wave's ds_read_b64 of one z from 32 rows spans
+// all 64 banks (as [row][4] it put rows r, r + 8, r + 16, r + 24 on one bank
+// pair: 4-way conflicts, 69% of the fp64 kernel's LDS cycles, profiles/r06_lds).
+template <typename R>
+__device__ __forceinline__ constexpr int xrow(int arr, int row)
+{
+    return sizeof(R) == 8 ? arr * 8 * MCEIK_XROWS + row : XROW(arr, 0, row);
+}
+template <typename R>
+__device__ __forceinline__ constexpr int xz(int z)
+{
+    return sizeof(R) == 8 ? z * MCEIK_XROWS : (z >> 2) * 4 * MCEIK_XROWS + (z & 3);
+}
+// the halo half this lane stages (slot 0 of it)
+template <typename R>
 __device__ __forceinline__ int halo_row_off(int lane)
 {
     const int j = lane >> 1, half = lane & 1;
-    return XROW((j >> 3) & 1, half, 64 + ((j >> 4) << 3) + (j & 7));
+    return xrow<R>((j >> 3) & 1, 64 + ((j >> 4) << 3) + (j & 7)) + xz<R>(4 * half);
 }
 template <typename R>
 __device__ __forceinline__ void store4(R *d, const R (&v)[4])
 {
 #pragma unroll
-    for (int i = 0; i < 4; i++) d[i] = v[i];
+    for (int i = 0; i < 4; i++) d[xz<R>(i)] = v[i];
 }
 template <typename R>
 __device__ __forceinline__ void store_row(R *x, int arr, int lane, const R (&v)[8])
 {
-    R *a = x + XROW(arr, 0, lane), *b = x + XROW(arr, 1, lane);
+    R *a = x + xrow<R>(arr, lane);
 #pragma unroll
-    for (int i = 0; i < 4; i++) { a[i] = v[i]; b[i] = v[4 + i]; }
+    for (int z = 0; z < 8; z++) a[xz<R>(z)] = v[z];
 }
 template <typename R>
-__device__ __forceinline__ void load_row(const R *x, int off0, R (&v)[8])   // off0 = XROW(arr, 0, row)
+__device__ __forceinline__ void load_row(const R *x, int off0, R (&v)[8])   // off0 = xrow(arr, row)
 {
-    const R *a = x + off0, *b = x + off0 + 4 * MCEIK_XROWS;
+    const R *a = x + off0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) { v[i] = a[i]; v[4 + i] = b[i]; }
+    for (int z = 0; z < 8; z++) v[z] = a[xz<R>(z)];
 }
 
 // Loads / stores that most lanes skip (z-upwind nodes of run starts, u0
@@ -296,7 +313,7 @@ __device__ __forceinline__ void pair_store(Rsrc r, uint32_t seg, bool chg, const
 // As fsm16's FL, with the held half in LDS instead of registers (this
 // instance runs at its VGPR limit).  Without it a line was read as two 64-B
 // halves a step apart and the L2 re-fetched part of them in between.
-#define XHOLD(k) (XROW(2, 0, 0) + (k) * 128)         // HOLD quarter k of lane l: 2 values at + 2 l
+#define XHOLD(k) (xrow<double>(2, 0) + (k) * 128)   // HOLD quarter k of lane l: 2 values at + 2 l
 __device__ __forceinline__ void line_issue64(Rsrc r, uint32_t lseg, bool isl, double (&a)[4], double (&h)[4],
                                              int &rowl, int &rowo)
 {
@@ -325,9 +342,9 @@ __device__ __forceinline__ void line_write64(double *x, int rowl, int rowo, cons
     double *hd = x + XHOLD(0) + 2 * lane;
     const double p0 = hd[0], p1 = hd[1], p2 = hd[128], p3 = hd[129];
     hd[0] = h[0]; hd[1] = h[1]; hd[128] = h[2]; hd[129] = h[3];
-    double *l = x + XROW(1, 0, rowl) + 2 * par, *o = x + XROW(1, 0, rowo) + 2 * par;
-    l[0] = a[0]; l[1] = a[1]; l[4 * MCEIK_XROWS] = a[2]; l[4 * MCEIK_XROWS + 1] = a[3];
-    o[0] = p0; o[1] = p1; o[4 * MCEIK_XROWS] = p2; o[4 * MCEIK_XROWS + 1] = p3;
+    double *l = x + xrow<double>(1, rowl) + xz<double>(2 * par), *o = x + xrow<double>(1, rowo) + xz<double>(2 * par);
+    l[0] = a[0]; l[xz<double>(1)] = a[1]; l[xz<double>(4)] = a[2]; l[xz<double>(5)] = a[3];
+    o[0] = p0; o[xz<double>(1)] = p1; o[xz<double>(4)] = p2; o[xz<double>(5)] = p3;
 }
 
 // Slowness of the 8 nodes of a segment (prefetch; multiplied by h when staged).
@@ -575,11 +592,11 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
     constexpr bool LAZY = sizeof(R) == 8;
     R xmr[8], xpr[8], ymr[8], ypr[8];
     const int lxs = lane & 7, lys = lane >> 3;
-    const int oxm = XROW(0, 0, lxs > 0 ? lane - 1 : 64 + lys), oym = XROW(0, 0, lys > 0 ? lane - 8 : 72 + lxs);
-    const int oxp = XROW(1, 0, lxs < 7 ? lane + 1 : 64 + lys), oyp = XROW(1, 0, lys < 7 ? lane + 8 : 72 + lxs);
+    const int oxm = xrow<R>(0, lxs > 0 ? lane - 1 : 64 + lys), oym = xrow<R>(0, lys > 0 ? lane - 8 : 72 + lxs);
+    const int oxp = xrow<R>(1, lxs < 7 ? lane + 1 : 64 + lys), oyp = xrow<R>(1, lys < 7 ? lane + 8 : 72 + lxs);
     // fp64: the next brick's first slot from this lane's XN row (the sweep
     // keeps no register copy of the next brick)
-    R nfirst = LAZY ? S.xr[XROW(1, RZ ? 1 : 0, lane) + (RZ ? 3 : 0)] : n[RZ ? 7 : 0];
+    R nfirst = LAZY ? S.xr[xrow<R>(1, lane) + xz<R>(RZ ? 7 : 0)] : n[RZ ? 7 : 0];
     if (zdsel) nfirst = zc;                  // held stream: a run end below the column end (HBM node)
     if (!LAZY) {
         load_row(S.xr, oxm, xmr);
@@ -597,7 +614,7 @@ __device__ __forceinline__ void brick_update(const FsmLaunch &L, const Smem<R, C
         const int pnext = RZ ? pj - 1 : pj + 1;
         const R self = c[pj];
         if (LAZY) {
-            const int sl = (pj & 3) + (pj >> 2) * 4 * MCEIK_XROWS;
+            const int sl = xz<R>(pj);
             xmr[pj] = S.xr[oxm + sl]; ymr[pj] = S.xr[oym + sl];
             xpr[pj] = S.xr[oxp + sl]; ypr[pj] = S.xr[oyp + sl];
         }
@@ -668,7 +685,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
     const int hj = lane >> 1, hh = lane & 1, he = halo_edge_lane(hj), hd = (he & 7) + (he >> 3);
     const unsigned hbit = hj < 16 ? C_XOWN : C_YOWN;
     const uint32_t hdelta = halo_delta(L, tile_bytes<R>(L), hj, he, rx, ry);
-    const int hso = halo_row_off(lane);
+    const int hso = halo_row_off<R>(lane);
     // column offsets inside a tile (the compact layout's cinfo_at): this lane's, the halo edge lane's
     const uint32_t lanecol = (uint32_t)colpos(lx, ly) * 128u;
     const uint32_t hcol = (uint32_t)colpos(rx ? 7 - (he & 7) : (he & 7), ry ? 7 - (he >> 3) : (he >> 3)) * 128u;
@@ -937,7 +954,7 @@ __device__ __forceinline__ int sweep(const FsmLaunch &L, Rsrc ur, Rsrc u0r, Rsrc
         constexpr bool LAZYN = sizeof(R) == 8;
         if (LAZYN) u0_store();
         store_row(S.xr, 0, lane, r);
-        if (LAZYN) load_row(S.xr, XROW(1, 0, lane), c);
+        if (LAZYN) load_row(S.xr, xrow<R>(1, lane), c);
         if (FL64)
             line_write64(reinterpret_cast<double *>(S.xr), rowl, rowo, la, lh);
         else
